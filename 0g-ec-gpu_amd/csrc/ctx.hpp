@@ -1,0 +1,97 @@
+// Internal runtime: device context, grow-only HBM workspace, error state and
+// per-kernel HIP-event timing.  Replaces the reference's per-call
+// Program::run closures (rust-gpu-tools) and ag-cuda-proxy's CudaWorkspace
+// (ag-cuda-proxy/src/module.rs:23-42): here one context = one device + one
+// stream + buffers that persist across calls (sized for 288 GB of HBM3E, so
+// 2^26-point MSMs and 2^24-point NTTs run as single chunks).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/ecgpu.h"
+
+namespace ecg {
+
+void set_error(const char* fmt, ...);
+
+#define ECG_HIP(call)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      ::ecg::set_error("HIP error %s (%s) at %s:%d", hipGetErrorName(e_),              \
+                       hipGetErrorString(e_), __FILE__, __LINE__);                      \
+      return ECG_ERR_HIP;                                                               \
+    }                                                                                   \
+  } while (0)
+
+#define ECG_TRY(expr)          \
+  do {                         \
+    int rc_ = (expr);          \
+    if (rc_ != ECG_OK) return rc_; \
+  } while (0)
+
+struct KernelTimes {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  double ms = 0.0;
+  int launches = 0;
+};
+
+}  // namespace ecg
+
+struct ecg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  size_t mem_bytes = 0;
+  int compute_units = 0;
+  struct Buf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+  };
+  std::map<std::string, Buf> ws;
+  // FFT twiddle-table cache key
+  int tw_fid = -1;
+  uint32_t tw_log_n = 0;
+  uint64_t tw_omega[4] = {0, 0, 0, 0};
+  // kernel timing (HIP events on the launch stream)
+  std::map<std::string, ecg::KernelTimes> ktimes;
+  std::vector<hipEvent_t> event_pool;
+};
+
+namespace ecg {
+
+// Make ctx's device current for this host thread.
+int ctx_enter(ecg_ctx* ctx);
+// Grow-only named device buffer.
+int ws_get(ecg_ctx* ctx, const char* name, size_t bytes, void** out);
+void ws_release(ecg_ctx* ctx, const char* name);
+
+// HIP-event bracket for one launch of a named kernel.
+hipEvent_t ev_take(ecg_ctx* ctx);
+void kt_reset(ecg_ctx* ctx, const char* name);
+int kt_begin(ecg_ctx* ctx, const char* name, hipStream_t s);
+int kt_end(ecg_ctx* ctx, const char* name, hipStream_t s);
+int kt_collect(ecg_ctx* ctx);  // after stream sync
+
+inline hipStream_t pick_stream(ecg_ctx* ctx, void* s) {
+  return s ? reinterpret_cast<hipStream_t>(s) : ctx->stream;
+}
+
+// Engine entry points (ntt.hip / msm.hip); data pointers are device memory.
+int ntt_run(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uint32_t log_n,
+            hipStream_t s, ecg_abort_cb abort_cb, void* user);
+int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n,
+            void* d_out_jac, hipStream_t s, ecg_abort_cb abort_cb, void* user);
+int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, void* d_out_jac,
+                  hipStream_t s);
+int gen_bases_run(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n,
+                  void* d_out, hipStream_t s);
+
+inline int fq_limbs64(int curve_id) { return curve_id == ECG_CURVE_BLS12_381 ? 6 : 4; }
+
+}  // namespace ecg

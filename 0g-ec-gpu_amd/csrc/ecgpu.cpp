@@ -1,0 +1,465 @@
+// C ABI of libecgpu.so (include/ecgpu.h): contexts, workspace, errors, the
+// host<->device boundary of the reference API, and multi-device dispatch.
+//
+// Reference mapping (ec-gpu-proxy):
+//   ecg_fft        <- SingleFftKernel::radix_fft        (src/fft.rs:50-135)
+//   ecg_fft_many   <- FftKernel::radix_fft_many         (src/fft.rs:211-246)
+//   ecg_msm        <- SingleMultiexpKernel::multiexp    (src/multiexp.rs:135-236)
+//   ecg_msm_multi  <- MultiexpKernel::parallel_multiexp (src/multiexp.rs:324-367)
+//                     + multiexp's device fold          (src/multiexp.rs:394-397)
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ctx.hpp"
+
+namespace ecg {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+int ctx_enter(ecg_ctx* ctx) {
+  if (!ctx) {
+    set_error("null context");
+    return ECG_ERR_INVALID;
+  }
+  ECG_HIP(hipSetDevice(ctx->device));
+  return ECG_OK;
+}
+
+int ws_get(ecg_ctx* ctx, const char* name, size_t bytes, void** out) {
+  auto& b = ctx->ws[name];
+  if (bytes == 0) bytes = 16;
+  if (b.bytes < bytes) {
+    if (b.ptr) {
+      // the buffer may still be in use by queued work
+      ECG_HIP(hipStreamSynchronize(ctx->stream));
+      ECG_HIP(hipFree(b.ptr));
+      b.ptr = nullptr;
+      b.bytes = 0;
+    }
+    hipError_t e = hipMalloc(&b.ptr, bytes);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("device allocation of %zu bytes for '%s' failed: %s", bytes, name, hipGetErrorString(e));
+      b.ptr = nullptr;
+      return ECG_ERR_NOMEM;
+    }
+    b.bytes = bytes;
+  }
+  *out = b.ptr;
+  return ECG_OK;
+}
+
+void ws_release(ecg_ctx* ctx, const char* name) {
+  auto it = ctx->ws.find(name);
+  if (it == ctx->ws.end()) return;
+  if (it->second.ptr) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(it->second.ptr);
+  }
+  ctx->ws.erase(it);
+}
+
+hipEvent_t ev_take(ecg_ctx* ctx) {
+  if (!ctx->event_pool.empty()) {
+    hipEvent_t e = ctx->event_pool.back();
+    ctx->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+void kt_reset(ecg_ctx* ctx, const char* name) {
+  auto& kt = ctx->ktimes[name];
+  for (auto& pr : kt.pending) {
+    ctx->event_pool.push_back(pr.first);
+    ctx->event_pool.push_back(pr.second);
+  }
+  kt.pending.clear();
+  kt.ms = 0.0;
+  kt.launches = 0;
+}
+
+int kt_begin(ecg_ctx* ctx, const char* name, hipStream_t s) {
+  hipEvent_t a = ev_take(ctx), b = ev_take(ctx);
+  if (!a || !b) {
+    set_error("hipEventCreate failed");
+    return ECG_ERR_HIP;
+  }
+  ECG_HIP(hipEventRecord(a, s));
+  ctx->ktimes[name].pending.push_back({a, b});
+  return ECG_OK;
+}
+
+int kt_end(ecg_ctx* ctx, const char* name, hipStream_t s) {
+  auto& kt = ctx->ktimes[name];
+  ECG_HIP(hipEventRecord(kt.pending.back().second, s));
+  return ECG_OK;
+}
+
+int kt_collect(ecg_ctx* ctx) {
+  for (auto& kv : ctx->ktimes) {
+    auto& kt = kv.second;
+    for (auto& pr : kt.pending) {
+      ECG_HIP(hipEventSynchronize(pr.second));
+      float ms = 0.f;
+      ECG_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+      kt.ms += ms;
+      kt.launches += 1;
+      ctx->event_pool.push_back(pr.first);
+      ctx->event_pool.push_back(pr.second);
+    }
+    kt.pending.clear();
+  }
+  return ECG_OK;
+}
+
+static size_t fr_bytes(int field_id) {
+  return (field_id == ECG_FIELD_BLS12_381_FQ) ? 48 : 32;
+}
+
+}  // namespace ecg
+
+using namespace ecg;
+
+extern "C" {
+
+const char* ecg_last_error(void) { return g_err.c_str(); }
+
+const char* ecg_version(void) { return "ecgpu-mi355x 0.1.0 (gfx950)"; }
+
+int ecg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int ecg_ctx_create(int device, ecg_ctx** out) {
+  if (!out) {
+    set_error("ecg_ctx_create: null out pointer");
+    return ECG_ERR_INVALID;
+  }
+  *out = nullptr;
+  int n = ecg_device_count();
+  if (n <= 0) {
+    set_error("No working GPUs found!");  // fft.rs:183, multiexp.rs:305
+    return ECG_ERR_NODEV;
+  }
+  if (device < 0 || device >= n) {
+    set_error("ecg_ctx_create: device %d out of range [0, %d)", device, n);
+    return ECG_ERR_INVALID;
+  }
+  ECG_HIP(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  ECG_HIP(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_error("ecg_ctx_create: device %d is %s; this build targets gfx950 (MI355X) only", device,
+              prop.gcnArchName);
+    return ECG_ERR_NODEV;
+  }
+  ecg_ctx* ctx = new ecg_ctx();
+  ctx->device = device;
+  ctx->mem_bytes = prop.totalGlobalMem;
+  ctx->compute_units = prop.multiProcessorCount;
+  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    set_error("hipStreamCreate failed: %s", hipGetErrorString(e));
+    delete ctx;
+    return ECG_ERR_HIP;
+  }
+  *out = ctx;
+  return ECG_OK;
+}
+
+void ecg_ctx_destroy(ecg_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->ws)
+    if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+  for (auto& kv : ctx->ktimes)
+    for (auto& pr : kv.second.pending) {
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+  for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int ecg_ctx_info(ecg_ctx* ctx, size_t* mem_bytes, int* compute_units) {
+  if (!ctx) {
+    set_error("null context");
+    return ECG_ERR_INVALID;
+  }
+  if (mem_bytes) *mem_bytes = ctx->mem_bytes;
+  if (compute_units) *compute_units = ctx->compute_units;
+  return ECG_OK;
+}
+
+// ---------------------------------------------------------------- FFT
+int ecg_fft_dev(ecg_ctx* ctx, int field_id, void* d_inout, const uint64_t* omega, uint32_t log_n, void* stream) {
+  ECG_TRY(ctx_enter(ctx));
+  if (!d_inout || !omega) {
+    set_error("ecg_fft_dev: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  hipStream_t s = pick_stream(ctx, stream);
+  ECG_TRY(ntt_run(ctx, field_id, d_inout, omega, log_n, s, nullptr, nullptr));
+  ECG_HIP(hipStreamSynchronize(s));
+  return kt_collect(ctx);
+}
+
+int ecg_fft(ecg_ctx* ctx, int field_id, uint64_t* inout, const uint64_t* omega, uint32_t log_n,
+            ecg_abort_cb abort_cb, void* user) {
+  ECG_TRY(ctx_enter(ctx));
+  if (!inout || !omega) {
+    set_error("ecg_fft: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  if (log_n > 32) {
+    set_error("radix_fft: log_n %u > 32 (LOG2_MAX_ELEMENTS, fft.rs:14)", log_n);
+    return ECG_ERR_INVALID;
+  }
+  const size_t bytes = ((size_t)1 << log_n) * fr_bytes(field_id);
+  void* d;
+  ECG_TRY(ws_get(ctx, "fft_io", bytes, &d));
+  hipStream_t s = ctx->stream;
+  ECG_HIP(hipMemcpyAsync(d, inout, bytes, hipMemcpyHostToDevice, s));  // fft.rs:89
+  int rc = ntt_run(ctx, field_id, d, omega, log_n, s, abort_cb, user);
+  if (rc != ECG_OK) {
+    (void)hipStreamSynchronize(s);
+    return rc;
+  }
+  ECG_HIP(hipMemcpyAsync(inout, d, bytes, hipMemcpyDeviceToHost, s));  // fft.rs:129
+  ECG_HIP(hipStreamSynchronize(s));
+  return kt_collect(ctx);
+}
+
+int ecg_fft_many(ecg_ctx** ctxs, int nctx, int field_id, uint64_t** inouts, const uint64_t* omegas,
+                 const uint32_t* log_ns, size_t count, ecg_abort_cb abort_cb, void* user) {
+  if (!ctxs || nctx <= 0) {
+    set_error("No working GPUs found!");
+    return ECG_ERR_NODEV;
+  }
+  if (count == 0) return ECG_OK;
+  const size_t chunk = (count + nctx - 1) / nctx;  // fft.rs:216
+  std::atomic<int> first_err{ECG_OK};
+  std::mutex mu;
+  std::string err_msg;
+  std::vector<std::thread> th;
+  for (int d = 0; d < nctx && (size_t)d * chunk < count; d++) {
+    th.emplace_back([&, d]() {
+      const size_t i0 = d * chunk, i1 = std::min(count, i0 + chunk);
+      for (size_t i = i0; i < i1; i++) {
+        if (first_err.load() != ECG_OK) break;  // fft.rs:233-235
+        int rc = ecg_fft(ctxs[d], field_id, inouts[i], omegas + 4 * i, log_ns[i], abort_cb, user);
+        if (rc != ECG_OK) {
+          int expected = ECG_OK;
+          if (first_err.compare_exchange_strong(expected, rc)) {
+            std::lock_guard<std::mutex> g(mu);
+            err_msg = g_err;
+          }
+          break;
+        }
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  if (first_err.load() != ECG_OK) g_err = err_msg;
+  return first_err.load();
+}
+
+// ---------------------------------------------------------------- MSM
+static int msm_host(ecg_ctx* ctx, int curve_id, const uint64_t* bases_xy, const uint64_t* scalars, size_t n,
+                    uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
+  ECG_TRY(ctx_enter(ctx));
+  if ((!bases_xy || !scalars) && n) {
+    set_error("ecg_msm: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  if (curve_id != ECG_CURVE_BLS12_381 && curve_id != ECG_CURVE_BN254) {
+    set_error("multiexp: unknown curve_id %d", curve_id);
+    return ECG_ERR_INVALID;
+  }
+  const size_t lq = fq_limbs64(curve_id);
+  const size_t bb = n * 2 * lq * 8, sb = n * 32, ob = 3 * lq * 8;
+  void *db, *ds, *dout;
+  ECG_TRY(ws_get(ctx, "msm_in_bases", bb, &db));
+  ECG_TRY(ws_get(ctx, "msm_in_scalars", sb, &ds));
+  ECG_TRY(ws_get(ctx, "msm_out", ob, &dout));
+  hipStream_t s = ctx->stream;
+  if (n) {
+    ECG_HIP(hipMemcpyAsync(db, bases_xy, bb, hipMemcpyHostToDevice, s));  // multiexp.rs:163-164
+    ECG_HIP(hipMemcpyAsync(ds, scalars, sb, hipMemcpyHostToDevice, s));
+  }
+  int rc = msm_run(ctx, curve_id, db, ds, n, dout, s, abort_cb, user);
+  if (rc != ECG_OK) {
+    (void)hipStreamSynchronize(s);
+    return rc;
+  }
+  ECG_HIP(hipMemcpyAsync(out_jac, dout, ob, hipMemcpyDeviceToHost, s));
+  ECG_HIP(hipStreamSynchronize(s));
+  return kt_collect(ctx);
+}
+
+int ecg_msm(ecg_ctx* ctx, int curve_id, const uint64_t* bases_xy, const uint64_t* scalars, size_t n,
+            uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
+  if (!out_jac) {
+    set_error("ecg_msm: null output");
+    return ECG_ERR_INVALID;
+  }
+  return msm_host(ctx, curve_id, bases_xy, scalars, n, out_jac, abort_cb, user);
+}
+
+int ecg_msm_dev(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, void* out_jac,
+                int out_on_device, void* stream) {
+  ECG_TRY(ctx_enter(ctx));
+  if (!out_jac || ((!d_bases || !d_scalars) && n)) {
+    set_error("ecg_msm_dev: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  if (curve_id != ECG_CURVE_BLS12_381 && curve_id != ECG_CURVE_BN254) {
+    set_error("multiexp: unknown curve_id %d", curve_id);
+    return ECG_ERR_INVALID;
+  }
+  hipStream_t s = pick_stream(ctx, stream);
+  const size_t ob = 3 * (size_t)fq_limbs64(curve_id) * 8;
+  void* dout = out_jac;
+  if (!out_on_device) ECG_TRY(ws_get(ctx, "msm_out", ob, &dout));
+  ECG_TRY(msm_run(ctx, curve_id, d_bases, d_scalars, n, dout, s, nullptr, nullptr));
+  if (!out_on_device) ECG_HIP(hipMemcpyAsync(out_jac, dout, ob, hipMemcpyDeviceToHost, s));
+  ECG_HIP(hipStreamSynchronize(s));
+  return kt_collect(ctx);
+}
+
+int ecg_point_sum_dev(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, uint64_t* out_jac,
+                      void* stream) {
+  ECG_TRY(ctx_enter(ctx));
+  if (!out_jac || (!d_points && count)) {
+    set_error("ecg_point_sum_dev: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  hipStream_t s = pick_stream(ctx, stream);
+  const size_t ob = 3 * (size_t)fq_limbs64(curve_id) * 8;
+  void* dout;
+  ECG_TRY(ws_get(ctx, "psum_out", ob, &dout));
+  ECG_TRY(point_sum_run(ctx, curve_id, d_points, count, dout, s));
+  ECG_HIP(hipMemcpyAsync(out_jac, dout, ob, hipMemcpyDeviceToHost, s));
+  ECG_HIP(hipStreamSynchronize(s));
+  return ECG_OK;
+}
+
+int ecg_msm_multi(ecg_ctx** ctxs, int nctx, int curve_id, const uint64_t* bases_xy, const uint64_t* scalars,
+                  size_t n, uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
+  if (!ctxs || nctx <= 0) {
+    set_error("No working GPUs found!");
+    return ECG_ERR_NODEV;
+  }
+  if (!out_jac) {
+    set_error("ecg_msm_multi: null output");
+    return ECG_ERR_INVALID;
+  }
+  const size_t lq = fq_limbs64(curve_id);
+  const size_t chunk = nctx > 0 ? (n + nctx - 1) / nctx : n;  // multiexp.rs:332-336
+  std::vector<uint64_t> partials((size_t)nctx * 3 * lq, 0);
+  std::atomic<int> first_err{ECG_OK};
+  std::mutex mu;
+  std::string err_msg;
+  std::vector<std::thread> th;
+  int used = 0;
+  for (int d = 0; d < nctx; d++) {
+    const size_t i0 = std::min(n, d * chunk), i1 = std::min(n, i0 + chunk);
+    if (d > 0 && i0 >= i1) break;
+    used++;
+    th.emplace_back([&, d, i0, i1]() {
+      int rc = msm_host(ctxs[d], curve_id, bases_xy + i0 * 2 * lq, scalars + i0 * 4, i1 - i0,
+                        partials.data() + (size_t)d * 3 * lq, abort_cb, user);
+      if (rc != ECG_OK) {
+        int expected = ECG_OK;
+        if (first_err.compare_exchange_strong(expected, rc)) {
+          std::lock_guard<std::mutex> g(mu);
+          err_msg = g_err;
+        }
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  if (first_err.load() != ECG_OK) {
+    g_err = err_msg;
+    return first_err.load();
+  }
+  if (used == 1) {
+    memcpy(out_jac, partials.data(), 3 * lq * 8);
+    return ECG_OK;
+  }
+  // cross-device fold on ctxs[0] (multiexp.rs:394-397)
+  ecg_ctx* c0 = ctxs[0];
+  ECG_TRY(ctx_enter(c0));
+  void* dp;
+  ECG_TRY(ws_get(c0, "multi_partials", (size_t)used * 3 * lq * 8, &dp));
+  ECG_HIP(hipMemcpyAsync(dp, partials.data(), (size_t)used * 3 * lq * 8, hipMemcpyHostToDevice, c0->stream));
+  return ecg_point_sum_dev(c0, curve_id, dp, used, out_jac, nullptr);
+}
+
+int ecg_msm_check_bases(int curve_id, const uint64_t* bases_xy, const uint64_t* scalars, size_t n) {
+  const size_t lq = fq_limbs64(curve_id);
+  for (size_t i = 0; i < n; i++) {
+    const uint64_t* e = scalars + 4 * i;
+    if ((e[0] | e[1] | e[2] | e[3]) == 0) continue;
+    uint64_t o = 0;
+    for (size_t k = 0; k < 2 * lq; k++) o |= bases_xy[i * 2 * lq + k];
+    if (o == 0) {
+      set_error("Encountered an identity element in the CRS.");
+      return ECG_ERR_INVALID;
+    }
+  }
+  return ECG_OK;
+}
+
+int ecg_gen_bases_dev(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n, void* d_out,
+                      void* stream) {
+  ECG_TRY(ctx_enter(ctx));
+  if (!a || !b || (!d_out && n)) {
+    set_error("ecg_gen_bases_dev: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  return gen_bases_run(ctx, curve_id, a, b, n, d_out, pick_stream(ctx, stream));
+}
+
+int ecg_last_kernel_time(ecg_ctx* ctx, const char* name, double* ms_total, int* launches) {
+  if (!ctx || !name) {
+    set_error("ecg_last_kernel_time: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  auto it = ctx->ktimes.find(name);
+  if (it == ctx->ktimes.end()) {
+    if (ms_total) *ms_total = 0;
+    if (launches) *launches = 0;
+    return ECG_OK;
+  }
+  if (ms_total) *ms_total = it->second.ms;
+  if (launches) *launches = it->second.launches;
+  return ECG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,456 @@
+"""Host-side mirror of the reference's ec-gpu-gen API over libecgpu.so.
+
+The reference (kriptohaberciniz/0g-ec-gpu) exposes this hot path to Rust
+provers as (ec-gpu-proxy/src/{fft,multiexp}.rs, ag-build/src/source/builder.rs,
+ec-gpu-program/src/program.rs):
+
+    let sb = ag_build::SourceBuilder::new().add_fft::<Fr>().add_multiexp::<G1Affine>();
+    ag_build::generate(&sb);                                   // build.rs
+    let programs = Device::all().iter().map(|d| program!(d)).collect()?;
+    let mut fft = FftKernel::<Fr>::create(programs)?;
+    fft.radix_fft_many(&mut [&mut coeffs], &[omega], &[log_n])?;
+    let mut msm = MultiexpKernel::<G1Affine>::create(programs, &devices)?;
+    let acc: G1Projective = msm.multiexp(&pool, bases, exps, skip)?;
+
+This module keeps those names, argument meanings and error behaviour, with
+numpy uint64 arrays in the arkworks in-memory layouts (see include/ecgpu.h):
+Fr elements (n, 4) Montgomery; bases (n, 2*Lq) [x|y] Montgomery (GpuRepr,
+identity = zeros); exps (n, 4) canonical BigInt<4>; results (3*Lq,) Jacobian.
+There is no CPU fallback: if libecgpu.so is missing this import fails.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from dataclasses import dataclass, field
+from typing import Callable, Optional, Sequence
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libecgpu.so")
+
+# ids shared with include/ecgpu.h
+FIELD_BLS12_381_FR, FIELD_BLS12_381_FQ, FIELD_BN254_FR, FIELD_BN254_FQ = 0, 1, 2, 3
+CURVE_BLS12_381, CURVE_BN254 = 0, 1
+FIELD_NAMES = {"bls12_381_fr": 0, "bls12_381_fq": 1, "bn254_fr": 2, "bn254_fq": 3}
+CURVE_NAMES = {"bls12_381": 0, "bn254": 1}
+CURVE_FQ_LIMBS = {0: 6, 1: 4}
+CURVE_FR_FIELD = {0: FIELD_BLS12_381_FR, 1: FIELD_BN254_FR}
+FR_TWO_ADICITY = {FIELD_BLS12_381_FR: 32, FIELD_BN254_FR: 28}
+
+ECG_OK, ECG_ABORTED = 0, 1
+ECG_ERR_INVALID, ECG_ERR_HIP, ECG_ERR_NOMEM, ECG_ERR_NODEV, ECG_ERR_RCCL = -1, -2, -3, -4, -5
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+ABORT_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+
+# ---------------------------------------------------------------------------
+# errors (ec-gpu-program/src/lib.rs:10-32)
+# ---------------------------------------------------------------------------
+
+
+class EcError(Exception):
+    """EcError::Simple / GpuTools / Io."""
+
+
+class Aborted(EcError):
+    """EcError::Aborted -- the maybe_abort callback returned true."""
+
+
+# ---------------------------------------------------------------------------
+# library loading (fails loudly: no CPU fallback on the product path)
+# ---------------------------------------------------------------------------
+
+_lib = None
+_lib_lock = threading.Lock()
+
+_SIGS = {
+    "ecg_device_count": (ctypes.c_int, []),
+    "ecg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "ecg_ctx_destroy": (None, [ctypes.c_void_p]),
+    "ecg_ctx_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int)]),
+    "ecg_last_error": (ctypes.c_char_p, []),
+    "ecg_version": (ctypes.c_char_p, []),
+    "ecg_fft": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, ctypes.c_uint32, ABORT_CB, ctypes.c_void_p]),
+    "ecg_fft_many": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int,
+                                    ctypes.POINTER(_u64p), _u64p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t,
+                                    ABORT_CB, ctypes.c_void_p]),
+    "ecg_fft_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, _u64p, ctypes.c_uint32, ctypes.c_void_p]),
+    "ecg_msm": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, ctypes.c_size_t, _u64p, ABORT_CB, ctypes.c_void_p]),
+    "ecg_msm_multi": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int, _u64p, _u64p,
+                                     ctypes.c_size_t, _u64p, ABORT_CB, ctypes.c_void_p]),
+    "ecg_msm_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "ecg_point_sum_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, _u64p,
+                                         ctypes.c_void_p]),
+    "ecg_msm_check_bases": (ctypes.c_int, [ctypes.c_int, _u64p, _u64p, ctypes.c_size_t]),
+    "ecg_gen_bases_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, ctypes.c_size_t,
+                                         ctypes.c_void_p, ctypes.c_void_p]),
+    "ecg_last_kernel_time": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_int)]),
+}
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"libecgpu.so not found at {LIB_PATH}: build the HIP extension "
+                    f"(`make -C 0g-ec-gpu_amd` or __graft_entry__.build()); there is no CPU fallback")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    return lib().ecg_last_error().decode(errors="replace")
+
+
+def _check(rc: int, what: str = ""):
+    if rc == ECG_OK:
+        return
+    if rc == ECG_ABORTED:
+        raise Aborted("GPU call was aborted!")
+    raise EcError(f"{what}: {last_error()} (rc={rc})" if what else f"{last_error()} (rc={rc})")
+
+
+def _ptr(a: np.ndarray):
+    if a.dtype != np.uint64 or not a.flags["C_CONTIGUOUS"]:
+        raise TypeError("expected a C-contiguous uint64 array")
+    return a.ctypes.data_as(_u64p)
+
+
+def _abort_cb(maybe_abort: Optional[Callable[[], bool]]):
+    if maybe_abort is None:
+        return ABORT_CB(0), None  # NULL function pointer
+    cb = ABORT_CB(lambda _user: 1 if maybe_abort() else 0)
+    return cb, cb  # keep a reference alive for the call
+
+
+# ---------------------------------------------------------------------------
+# SourceBuilder / generate (ag-build/src/source/builder.rs, ag-build/src/lib.rs)
+# Kernels are prebuilt for gfx950; the builder records which field/curve
+# instantiations a downstream build asked for, and generate() checks that the
+# prebuilt library provides them (there is no runtime codegen / nvcc step).
+# ---------------------------------------------------------------------------
+
+
+@dataclass
+class SourceBuilder:
+    fields: set = field(default_factory=set)
+    ffts: set = field(default_factory=set)
+    ecs: set = field(default_factory=set)
+    ec_ffts: set = field(default_factory=set)
+    multiexps: set = field(default_factory=set)
+    extra_sources: list = field(default_factory=list)
+
+    @staticmethod
+    def new() -> "SourceBuilder":
+        return SourceBuilder()
+
+    def add_field(self, f: str) -> "SourceBuilder":
+        self.fields.add(f)
+        return self
+
+    def add_fft(self, f: str) -> "SourceBuilder":
+        self.add_field(f)
+        self.ffts.add(f)
+        return self
+
+    def add_ec(self, curve: str) -> "SourceBuilder":
+        self.add_field(curve + "_fq").add_field(curve + "_fr")
+        self.ecs.add(curve)
+        return self
+
+    def add_ec_fft(self, curve: str) -> "SourceBuilder":
+        self.add_ec(curve)
+        self.ec_ffts.add(curve)
+        return self
+
+    def add_multiexp(self, curve: str) -> "SourceBuilder":
+        self.add_ec(curve)
+        self.multiexps.add(curve)
+        return self
+
+    def append_source(self, source: str) -> "SourceBuilder":
+        self.extra_sources.append(source)
+        return self
+
+    def build_32_bit_limbs(self) -> str:
+        return self._describe(32)
+
+    def build_64_bit_limbs(self) -> str:
+        return self._describe(64)
+
+    def _describe(self, limb_bits: int) -> str:
+        return "\n".join([f"// prebuilt gfx950 kernels, {limb_bits}-bit host limbs"]
+                         + [f"// fft {f}" for f in sorted(self.ffts)]
+                         + [f"// multiexp {c}" for c in sorted(self.multiexps)])
+
+
+def generate(sb: SourceBuilder) -> None:
+    """ag_build::generate: validates that every requested instantiation is in
+    the prebuilt library (field/curve ids) and that the library loads."""
+    for f in sb.ffts:
+        if f not in ("bls12_381_fr", "bn254_fr"):
+            raise EcError(f"no prebuilt FFT for field {f!r}")
+    for c in sb.multiexps:
+        if c not in CURVE_NAMES:
+            raise EcError(f"no prebuilt multiexp for curve {c!r}")
+    if sb.ec_ffts:
+        raise EcError("G1 EC-FFT (add_ec_fft) is not part of this build (SURVEY §8f next #2)")
+    lib()
+
+
+# ---------------------------------------------------------------------------
+# Device / Program (rust_gpu_tools::Device, ec_gpu_program::program!)
+# ---------------------------------------------------------------------------
+
+
+class Device:
+    def __init__(self, index: int):
+        self.index = index
+
+    @staticmethod
+    def all() -> list["Device"]:
+        return [Device(i) for i in range(lib().ecg_device_count())]
+
+    def name(self) -> str:
+        return f"MI355X #{self.index} (gfx950)"
+
+
+class Program:
+    """One context per device: device, stream, persistent HBM workspace."""
+
+    def __init__(self, device: Device):
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(lib().ecg_ctx_create(device.index, ctypes.byref(h)), "program!")
+        self.handle = h
+        self._lock = threading.Lock()
+
+    def device_name(self) -> str:
+        return self.device.name()
+
+    def memory(self) -> int:
+        mem = ctypes.c_size_t()
+        cus = ctypes.c_int()
+        _check(lib().ecg_ctx_info(self.handle, ctypes.byref(mem), ctypes.byref(cus)))
+        return mem.value
+
+    def compute_units(self) -> int:
+        mem = ctypes.c_size_t()
+        cus = ctypes.c_int()
+        _check(lib().ecg_ctx_info(self.handle, ctypes.byref(mem), ctypes.byref(cus)))
+        return cus.value
+
+    def kernel_time(self, name: str) -> tuple[float, int]:
+        ms = ctypes.c_double()
+        cnt = ctypes.c_int()
+        _check(lib().ecg_last_kernel_time(self.handle, name.encode(), ctypes.byref(ms), ctypes.byref(cnt)))
+        return ms.value, cnt.value
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().ecg_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def program(device: Device) -> Program:
+    """ec_gpu_program::program!(device)."""
+    return Program(device)
+
+
+load_program = program  # ec_gpu_program::load_program! (test-tools)
+
+
+# ---------------------------------------------------------------------------
+# FFT (ec-gpu-proxy/src/fft.rs)
+# ---------------------------------------------------------------------------
+
+
+def _fft_field(f) -> int:
+    fid = FIELD_NAMES.get(f, f) if isinstance(f, str) else int(f)
+    if fid not in (FIELD_BLS12_381_FR, FIELD_BN254_FR):
+        raise EcError(f"FftKernel: unsupported field {f!r}")
+    return fid
+
+
+class SingleFftKernel:
+    def __init__(self, prog: Program, fid: int, maybe_abort=None):
+        self.program = prog
+        self.fid = fid
+        self.maybe_abort = maybe_abort
+
+    def radix_fft(self, inp: np.ndarray, omega: np.ndarray, log_n: int) -> None:
+        """In place: inp (2^log_n, 4) uint64 Montgomery."""
+        if inp.shape != (1 << log_n, 4):
+            raise EcError(f"radix_fft: expected shape {(1 << log_n, 4)}, got {inp.shape}")
+        om = np.ascontiguousarray(omega, dtype=np.uint64).reshape(4)
+        cb, keep = _abort_cb(self.maybe_abort)
+        with self.program._lock:
+            rc = lib().ecg_fft(self.program.handle, self.fid, _ptr(inp), _ptr(om), log_n, cb, None)
+        del keep
+        _check(rc, "radix_fft")
+
+
+class FftKernel:
+    """One FFT kernel per device (fft.rs:139-246)."""
+
+    def __init__(self, kernels: list[SingleFftKernel]):
+        self.kernels = kernels
+
+    @staticmethod
+    def create(programs: Sequence[Program], field: str | int = "bls12_381_fr") -> "FftKernel":
+        return FftKernel._create(programs, field, None)
+
+    @staticmethod
+    def create_with_abort(programs, maybe_abort: Callable[[], bool], field: str | int = "bls12_381_fr"):
+        return FftKernel._create(programs, field, maybe_abort)
+
+    @staticmethod
+    def _create(programs, field, maybe_abort):
+        fid = _fft_field(field)
+        kernels = [SingleFftKernel(p, fid, maybe_abort) for p in programs]
+        if not kernels:
+            raise EcError("No working GPUs found!")
+        return FftKernel(kernels)
+
+    def radix_fft(self, inp: np.ndarray, omega: np.ndarray, log_n: int) -> None:
+        """Uses the first GPU (fft.rs:200-204)."""
+        self.kernels[0].radix_fft(inp, omega, log_n)
+
+    def radix_fft_many(self, inputs: Sequence[np.ndarray], omegas: Sequence[np.ndarray],
+                       log_ns: Sequence[int]) -> None:
+        """ceil(m / #devices) chunks, one host thread per device, first error
+        wins and stops the other workers at their next input (fft.rs:211-246)."""
+        n = len(inputs)
+        if not (len(omegas) == n and len(log_ns) == n):
+            raise EcError("radix_fft_many: inputs/omegas/log_ns length mismatch")
+        if n == 0:
+            return
+        for a, ln in zip(inputs, log_ns):
+            if a.shape != (1 << ln, 4) or a.dtype != np.uint64 or not a.flags["C_CONTIGUOUS"]:
+                raise EcError("radix_fft_many: each input must be a C-contiguous (2^log_n, 4) uint64 array")
+        nd = len(self.kernels)
+        ctxs = (ctypes.c_void_p * nd)(*[k.program.handle.value for k in self.kernels])
+        ptrs = (_u64p * n)(*[_ptr(a) for a in inputs])
+        om = np.ascontiguousarray(np.stack([np.asarray(o, dtype=np.uint64).reshape(4) for o in omegas]))
+        lns = (ctypes.c_uint32 * n)(*log_ns)
+        cb, keep = _abort_cb(self.kernels[0].maybe_abort)
+        rc = lib().ecg_fft_many(ctxs, nd, self.kernels[0].fid, ptrs, _ptr(om), lns, n, cb, None)
+        del keep
+        _check(rc, "radix_fft_many")
+
+
+# ---------------------------------------------------------------------------
+# Multiexp (ec-gpu-proxy/src/multiexp.rs)
+# ---------------------------------------------------------------------------
+
+
+class Worker:
+    """threadpool::Worker stand-in (the device work is dispatched by the C++
+    library with one host thread per device)."""
+
+    def __init__(self, num_threads: Optional[int] = None):
+        env = os.environ.get("EC_GPU_NUM_THREADS")
+        self.num_threads = num_threads or (int(env) if env and env.isdigit() else (os.cpu_count() or 1))
+
+    def log_num_threads(self) -> int:
+        return max(0, self.num_threads.bit_length() - 1)
+
+
+def _curve(c) -> int:
+    cid = CURVE_NAMES.get(c, c) if isinstance(c, str) else int(c)
+    if cid not in CURVE_FQ_LIMBS:
+        raise EcError(f"MultiexpKernel: unsupported curve {c!r}")
+    return cid
+
+
+class SingleMultiexpKernel:
+    def __init__(self, prog: Program, cid: int, maybe_abort=None):
+        self.program = prog
+        self.cid = cid
+        self.maybe_abort = maybe_abort
+        self.n = 1 << 31  # terms per call the device handles (calc_chunk_size analogue)
+
+    def multiexp(self, bases: np.ndarray, exps: np.ndarray) -> np.ndarray:
+        lq = CURVE_FQ_LIMBS[self.cid]
+        if bases.shape[0] != exps.shape[0]:
+            raise EcError("multiexp: bases and exponents differ in length")
+        b = np.ascontiguousarray(bases, dtype=np.uint64).reshape(-1, 2 * lq)
+        e = np.ascontiguousarray(exps, dtype=np.uint64).reshape(-1, 4)
+        out = np.zeros(3 * lq, dtype=np.uint64)
+        cb, keep = _abort_cb(self.maybe_abort)
+        with self.program._lock:
+            rc = lib().ecg_msm(self.program.handle, self.cid, _ptr(b), _ptr(e), e.shape[0], _ptr(out), cb, None)
+        del keep
+        _check(rc, "multiexp")
+        return out
+
+
+class MultiexpKernel:
+    """Multiexp kernels for several devices (multiexp.rs:256-404)."""
+
+    def __init__(self, kernels: list[SingleMultiexpKernel]):
+        self.kernels = kernels
+
+    @staticmethod
+    def create(programs: Sequence[Program], devices: Sequence[Device] = (), curve: str | int = "bls12_381"):
+        return MultiexpKernel._create(programs, curve, None)
+
+    @staticmethod
+    def create_with_abort(programs, devices, maybe_abort: Callable[[], bool], curve: str | int = "bls12_381"):
+        return MultiexpKernel._create(programs, curve, maybe_abort)
+
+    @staticmethod
+    def _create(programs, curve, maybe_abort):
+        cid = _curve(curve)
+        kernels = [SingleMultiexpKernel(p, cid, maybe_abort) for p in programs]
+        if not kernels:
+            raise EcError("No working GPUs found!")
+        return MultiexpKernel(kernels)
+
+    def num_kernels(self) -> int:
+        return len(self.kernels)
+
+    def multiexp(self, pool: Worker, bases: np.ndarray, exps: np.ndarray, skip: int = 0) -> np.ndarray:
+        """sum_i exps[i] * bases[skip + i]  ->  Jacobian (3*Lq,) uint64."""
+        cid = self.kernels[0].cid
+        lq = CURVE_FQ_LIMBS[cid]
+        e = np.ascontiguousarray(exps, dtype=np.uint64).reshape(-1, 4)
+        n = e.shape[0]
+        if skip + n > bases.shape[0]:
+            raise EcError("multiexp: Expected more bases from source.")
+        b = np.ascontiguousarray(bases[skip:skip + n], dtype=np.uint64).reshape(-1, 2 * lq)
+        out = np.zeros(3 * lq, dtype=np.uint64)
+        nd = len(self.kernels)
+        ctxs = (ctypes.c_void_p * nd)(*[k.program.handle.value for k in self.kernels])
+        cb, keep = _abort_cb(self.kernels[0].maybe_abort)
+        rc = lib().ecg_msm_multi(ctxs, nd, cid, _ptr(b), _ptr(e), n, _ptr(out), cb, None)
+        del keep
+        _check(rc, "multiexp")
+        return out
+
+
+def check_bases(curve, bases: np.ndarray, exps: np.ndarray) -> None:
+    """Raise EcError like multiexp_cpu.rs:57-61 if a base with a non-zero
+    exponent is the identity."""
+    cid = _curve(curve)
+    b = np.ascontiguousarray(bases, dtype=np.uint64)
+    e = np.ascontiguousarray(exps, dtype=np.uint64)
+    _check(lib().ecg_msm_check_bases(cid, _ptr(b), _ptr(e), e.size // 4), "multiexp")

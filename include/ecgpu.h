@@ -1,0 +1,146 @@
+/*
+ * ecgpu.h -- C ABI of the MI355X-native MSM + radix-FFT engine (libecgpu.so).
+ *
+ * This is the drop-in boundary for the reference's ec-gpu-gen host API
+ * (kriptohaberciniz/0g-ec-gpu, crate ec-gpu-proxy).  A thin binding (the Rust
+ * shim in INTEGRATION.md, or the Python mirror in 0g-ec-gpu_amd/ecgpu/) keeps
+ * the reference's types and calls these functions; no rust-gpu-tools, no
+ * CUDA/OpenCL dispatch.  Signatures use plain pointers and sizes only.
+ *
+ * Element layouts are exactly the arkworks 0.4 in-memory layouts the
+ * reference passes around:
+ *   field element  : N little-endian u64 limbs, Montgomery form, R = 2^(64N),
+ *                    fully reduced (ark_ff::Fp<MontBackend<_,N>,N>);
+ *                    Fr: N = 4 (32 B); BLS12-381 Fq: N = 6 (48 B); BN254 Fq: N = 4.
+ *   scalar (exp)   : BigInt<4>, canonical little-endian u64 limbs (32 B)
+ *                    (PrimeFieldRepr::to_bigint, ag-types/src/impls.rs:7-18).
+ *   base           : [x, y] Montgomery, identity = all zero
+ *                    (GpuRepr::to_gpu_repr, ag-types/src/impls.rs:48-58).
+ *   result point   : Jacobian [X, Y, Z] Montgomery (G::Curve), normalised:
+ *                    (x, y, 1) or the identity (0, 1, 0).
+ *
+ * Return codes: 0 = ok, 1 = aborted (EcError::Aborted), < 0 = error
+ * (EcError::Simple / GpuTools); ecg_last_error() gives the thread's message.
+ * All calls are synchronous and thread-safe for distinct contexts.
+ */
+#ifndef ECGPU_H
+#define ECGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- ids ------------------------------------------------------------- */
+#define ECG_FIELD_BLS12_381_FR 0
+#define ECG_FIELD_BLS12_381_FQ 1
+#define ECG_FIELD_BN254_FR 2
+#define ECG_FIELD_BN254_FQ 3
+
+#define ECG_CURVE_BLS12_381 0 /* G1 over BLS12-381 Fq, scalars in Fr */
+#define ECG_CURVE_BN254 1     /* G1 over BN254 Fq, scalars in Fr      */
+
+#define ECG_OK 0
+#define ECG_ABORTED 1
+#define ECG_ERR_INVALID (-1)  /* bad argument (EcError::Simple)            */
+#define ECG_ERR_HIP (-2)      /* HIP runtime error (EcError::GpuTools)     */
+#define ECG_ERR_NOMEM (-3)    /* device allocation failed                  */
+#define ECG_ERR_NODEV (-4)    /* "No working GPUs found!"                  */
+#define ECG_ERR_RCCL (-5)     /* collective failed                         */
+
+/* Polled between FFT passes / MSM chunks; non-zero => abort
+ * (the reference's maybe_abort: &dyn Fn() -> bool, fft.rs:94-98,
+ * multiexp.rs:140-144). */
+typedef int (*ecg_abort_cb)(void *user);
+
+typedef struct ecg_ctx ecg_ctx;
+
+/* ---- devices and contexts ---------------------------------------------
+ * Replace rust_gpu_tools::Device::all() + ec_gpu_program::program!(device)
+ * (ec-gpu-program/src/program.rs:11-29, 97-106).  A context owns one HIP
+ * device, one stream and a grow-only device workspace (twiddle tables,
+ * MSM bucket arrays) that persists across calls. */
+int ecg_device_count(void);
+int ecg_ctx_create(int device, ecg_ctx **out);
+void ecg_ctx_destroy(ecg_ctx *ctx);
+/* device memory and compute units (Device::memory / compute_units,
+ * used by multiexp.rs:109-127) */
+int ecg_ctx_info(ecg_ctx *ctx, size_t *mem_bytes, int *compute_units);
+const char *ecg_last_error(void);
+const char *ecg_version(void);
+
+/* ---- FFT ----------------------------------------------------------------
+ * In-place forward DFT of size 2^log_n over field_id (an Fr), natural order
+ * in and out, no 1/n scaling: a[k] <- sum_j a[j] * omega^(j k).
+ * Replaces SingleFftKernel::radix_fft (ec-gpu-proxy/src/fft.rs:50-135) and
+ * FftKernel::radix_fft (fft.rs:200-204).  log_n = 0 is rejected
+ * (the reference panics, fft.rs:68-70); log_n <= the field's 2-adicity. */
+int ecg_fft(ecg_ctx *ctx, int field_id, uint64_t *inout, const uint64_t *omega, uint32_t log_n,
+            ecg_abort_cb abort_cb, void *user);
+
+/* FftKernel::radix_fft_many (fft.rs:211-246): `count` transforms
+ * distributed in ceil(count / nctx) chunks, one host thread per context,
+ * first error wins. */
+int ecg_fft_many(ecg_ctx **ctxs, int nctx, int field_id, uint64_t **inouts, const uint64_t *omegas,
+                 const uint32_t *log_ns, size_t count, ecg_abort_cb abort_cb, void *user);
+
+/* Device-resident variant: d_inout is a device pointer on ctx's device
+ * (n x 32 B); `stream` is a hipStream_t (NULL = the context's stream).
+ * Inputs stay in HBM; used by bench.py and by callers that keep
+ * polynomials resident. */
+int ecg_fft_dev(ecg_ctx *ctx, int field_id, void *d_inout, const uint64_t *omega, uint32_t log_n,
+                void *stream);
+
+/* ---- MSM ------------------------------------------------------------------
+ * out = sum_{i<n} scalars[i] * bases[i] on curve_id's G1.
+ * Replaces SingleMultiexpKernel::multiexp (ec-gpu-proxy/src/multiexp.rs:135-236)
+ * and MultiexpKernel::multiexp (multiexp.rs:372-400, called with
+ * bases + skip already applied).  Identity bases contribute nothing (the
+ * reference CPU path rejects them, multiexp_cpu.rs:57-61; use
+ * ecg_msm_check_bases to reproduce that error).  Any 256-bit scalar is
+ * accepted and reduced mod r (same group element as multiexp_cpu). */
+int ecg_msm(ecg_ctx *ctx, int curve_id, const uint64_t *bases_xy, const uint64_t *scalars, size_t n,
+            uint64_t *out_jac, ecg_abort_cb abort_cb, void *user);
+
+/* MultiexpKernel::parallel_multiexp + multiexp (multiexp.rs:324-400):
+ * contiguous ceil(n / nctx) ranges, one host thread per context, partial
+ * sums folded on the device of ctxs[0]. */
+int ecg_msm_multi(ecg_ctx **ctxs, int nctx, int curve_id, const uint64_t *bases_xy,
+                  const uint64_t *scalars, size_t n, uint64_t *out_jac, ecg_abort_cb abort_cb,
+                  void *user);
+
+/* Device-resident variant (cf. ag_cuda_ec::multiexp::upload_multiexp_bases,
+ * ag-cuda-ec/src/multiexp.rs:11-19): d_bases / d_scalars are device
+ * pointers on ctx's device.  out_jac is host memory (3 x Lq u64) or, with
+ * out_on_device != 0, a device pointer. */
+int ecg_msm_dev(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n,
+                void *out_jac, int out_on_device, void *stream);
+
+/* Sum `count` Jacobian points (3 x Lq u64 each, device memory) into one
+ * normalised Jacobian point: the EC fold that follows the RCCL all-gather of
+ * per-GPU partials (RCCL has no EC-add reduction op).  out is host memory. */
+int ecg_point_sum_dev(ecg_ctx *ctx, int curve_id, const void *d_points, size_t count,
+                      uint64_t *out_jac, void *stream);
+
+/* Returns ECG_ERR_INVALID with "Encountered an identity element in the
+ * CRS." if any base with a non-zero scalar is the identity -- the
+ * reference CPU path's error behaviour (multiexp_cpu.rs:57-61). */
+int ecg_msm_check_bases(int curve_id, const uint64_t *bases_xy, const uint64_t *scalars, size_t n);
+
+/* ---- synthetic inputs for benchmarks/tests (not part of the reference API)
+ * Bases P_i = (a + i*b) * G for i < n written to device memory d_out
+ * (n x 2 x Lq u64, GpuRepr layout); a, b canonical 4-limb scalars. */
+int ecg_gen_bases_dev(ecg_ctx *ctx, int curve_id, const uint64_t *a, const uint64_t *b, size_t n,
+                      void *d_out, void *stream);
+
+/* Kernel timing of the most recent call on this context (ms per launch of
+ * the dominant kernel, and its launch count), recorded with HIP events on
+ * the stream the kernels ran on.  name is "ntt_pass" or "msm_accumulate". */
+int ecg_last_kernel_time(ecg_ctx *ctx, const char *name, double *ms_total, int *launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ECGPU_H */
