@@ -83,12 +83,16 @@ inline hipStream_t pick_stream(ecg_ctx* ctx, void* s) {
 }
 
 // Engine entry points (ntt.hip / msm.hip); data pointers are device memory.
+int ntt_validate(int field_id, uint32_t log_n);
 int ntt_run(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uint32_t log_n,
             hipStream_t s, ecg_abort_cb abort_cb, void* user);
+// MSM / point-sum results are written to HOST memory (3 x Lq u64, normalised
+// Jacobian): the last serial steps (window fold, normalisation) run on the host.
 int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n,
-            void* d_out_jac, hipStream_t s, ecg_abort_cb abort_cb, void* user);
-int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, void* d_out_jac,
+            uint64_t* out_jac, hipStream_t s, ecg_abort_cb abort_cb, void* user);
+int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, uint64_t* out_jac,
                   hipStream_t s);
+int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac);
 int gen_bases_run(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n,
                   void* d_out, hipStream_t s);
 

@@ -21,6 +21,7 @@ template <class FqP, class FrP, class GenP>
 struct CurveCfg {
   using Fq = Fp<FqP>;
   using Fr = Fp<FrP>;
+  using FqParams = FqP;
   using FrParams = FrP;
   using Gen = GenP;
 };

@@ -236,10 +236,7 @@ int ecg_fft(ecg_ctx* ctx, int field_id, uint64_t* inout, const uint64_t* omega, 
     set_error("ecg_fft: null pointer");
     return ECG_ERR_INVALID;
   }
-  if (log_n > 32) {
-    set_error("radix_fft: log_n %u > 32 (LOG2_MAX_ELEMENTS, fft.rs:14)", log_n);
-    return ECG_ERR_INVALID;
-  }
+  ECG_TRY(ntt_validate(field_id, log_n));  // before any allocation or copy
   const size_t bytes = ((size_t)1 << log_n) * fr_bytes(field_id);
   void* d;
   ECG_TRY(ws_get(ctx, "fft_io", bytes, &d));
@@ -302,23 +299,18 @@ static int msm_host(ecg_ctx* ctx, int curve_id, const uint64_t* bases_xy, const 
     return ECG_ERR_INVALID;
   }
   const size_t lq = fq_limbs64(curve_id);
-  const size_t bb = n * 2 * lq * 8, sb = n * 32, ob = 3 * lq * 8;
-  void *db, *ds, *dout;
+  const size_t bb = n * 2 * lq * 8, sb = n * 32;
+  void *db, *ds;
   ECG_TRY(ws_get(ctx, "msm_in_bases", bb, &db));
   ECG_TRY(ws_get(ctx, "msm_in_scalars", sb, &ds));
-  ECG_TRY(ws_get(ctx, "msm_out", ob, &dout));
   hipStream_t s = ctx->stream;
   if (n) {
     ECG_HIP(hipMemcpyAsync(db, bases_xy, bb, hipMemcpyHostToDevice, s));  // multiexp.rs:163-164
     ECG_HIP(hipMemcpyAsync(ds, scalars, sb, hipMemcpyHostToDevice, s));
   }
-  int rc = msm_run(ctx, curve_id, db, ds, n, dout, s, abort_cb, user);
-  if (rc != ECG_OK) {
-    (void)hipStreamSynchronize(s);
-    return rc;
-  }
-  ECG_HIP(hipMemcpyAsync(out_jac, dout, ob, hipMemcpyDeviceToHost, s));
-  ECG_HIP(hipStreamSynchronize(s));
+  int rc = msm_run(ctx, curve_id, db, ds, n, out_jac, s, abort_cb, user);
+  (void)hipStreamSynchronize(s);
+  if (rc != ECG_OK) return rc;
   return kt_collect(ctx);
 }
 
@@ -343,11 +335,14 @@ int ecg_msm_dev(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_s
     return ECG_ERR_INVALID;
   }
   hipStream_t s = pick_stream(ctx, stream);
+  uint64_t host_out[18];
   const size_t ob = 3 * (size_t)fq_limbs64(curve_id) * 8;
-  void* dout = out_jac;
-  if (!out_on_device) ECG_TRY(ws_get(ctx, "msm_out", ob, &dout));
-  ECG_TRY(msm_run(ctx, curve_id, d_bases, d_scalars, n, dout, s, nullptr, nullptr));
-  if (!out_on_device) ECG_HIP(hipMemcpyAsync(out_jac, dout, ob, hipMemcpyDeviceToHost, s));
+  ECG_TRY(msm_run(ctx, curve_id, d_bases, d_scalars, n, host_out, s, nullptr, nullptr));
+  if (out_on_device) {
+    ECG_HIP(hipMemcpyAsync(out_jac, host_out, ob, hipMemcpyHostToDevice, s));
+  } else {
+    memcpy(out_jac, host_out, ob);
+  }
   ECG_HIP(hipStreamSynchronize(s));
   return kt_collect(ctx);
 }
@@ -359,13 +354,44 @@ int ecg_point_sum_dev(ecg_ctx* ctx, int curve_id, const void* d_points, size_t c
     set_error("ecg_point_sum_dev: null pointer");
     return ECG_ERR_INVALID;
   }
-  hipStream_t s = pick_stream(ctx, stream);
-  const size_t ob = 3 * (size_t)fq_limbs64(curve_id) * 8;
-  void* dout;
-  ECG_TRY(ws_get(ctx, "psum_out", ob, &dout));
-  ECG_TRY(point_sum_run(ctx, curve_id, d_points, count, dout, s));
-  ECG_HIP(hipMemcpyAsync(out_jac, dout, ob, hipMemcpyDeviceToHost, s));
-  ECG_HIP(hipStreamSynchronize(s));
+  return point_sum_run(ctx, curve_id, d_points, count, out_jac, pick_stream(ctx, stream));
+}
+
+// ---------------------------------------------------------------- device buffers
+int ecg_dev_alloc(ecg_ctx* ctx, size_t bytes, void** out) {
+  ECG_TRY(ctx_enter(ctx));
+  if (!out) {
+    set_error("ecg_dev_alloc: null out pointer");
+    return ECG_ERR_INVALID;
+  }
+  hipError_t e = hipMalloc(out, bytes ? bytes : 16);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("device allocation of %zu bytes failed: %s", bytes, hipGetErrorString(e));
+    *out = nullptr;
+    return ECG_ERR_NOMEM;
+  }
+  return ECG_OK;
+}
+
+void ecg_dev_free(ecg_ctx* ctx, void* p) {
+  if (!ctx || !p) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipFree(p);
+}
+
+int ecg_dev_upload(ecg_ctx* ctx, void* d_dst, const void* src, size_t bytes) {
+  ECG_TRY(ctx_enter(ctx));
+  ECG_HIP(hipMemcpyAsync(d_dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  ECG_HIP(hipStreamSynchronize(ctx->stream));
+  return ECG_OK;
+}
+
+int ecg_dev_download(ecg_ctx* ctx, void* dst, const void* d_src, size_t bytes) {
+  ECG_TRY(ctx_enter(ctx));
+  ECG_HIP(hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  ECG_HIP(hipStreamSynchronize(ctx->stream));
   return ECG_OK;
 }
 
@@ -412,13 +438,16 @@ int ecg_msm_multi(ecg_ctx** ctxs, int nctx, int curve_id, const uint64_t* bases_
     memcpy(out_jac, partials.data(), 3 * lq * 8);
     return ECG_OK;
   }
-  // cross-device fold on ctxs[0] (multiexp.rs:394-397)
-  ecg_ctx* c0 = ctxs[0];
-  ECG_TRY(ctx_enter(c0));
-  void* dp;
-  ECG_TRY(ws_get(c0, "multi_partials", (size_t)used * 3 * lq * 8, &dp));
-  ECG_HIP(hipMemcpyAsync(dp, partials.data(), (size_t)used * 3 * lq * 8, hipMemcpyHostToDevice, c0->stream));
-  return ecg_point_sum_dev(c0, curve_id, dp, used, out_jac, nullptr);
+  // cross-device fold of the per-device partials (multiexp.rs:394-397)
+  return point_sum_host(curve_id, partials.data(), used, out_jac);
+}
+
+int ecg_point_sum(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac) {
+  if (!out_jac || (!points && count)) {
+    set_error("ecg_point_sum: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  return point_sum_host(curve_id, points, count, out_jac);
 }
 
 int ecg_msm_check_bases(int curve_id, const uint64_t* bases_xy, const uint64_t* scalars, size_t n) {

@@ -14,27 +14,40 @@
 //                     (hipcub/rocPRIM onesweep).  Replaces the reference's
 //                     per-thread global-memory bucket RMW (multiexp_backup.cl:45-58).
 //  3. msm_bounds      bucket -> [start, end) in the sorted array.
-//  4. msm_accumulate  one thread per bucket: XYZZ mixed adds (8M+2S) of the
-//                     gathered affine bases (negated for negative digits).
+//  4. msm_accumulate  fixed-length segments of SEG sorted entries per thread
+//                     (every lane runs exactly SEG XYZZ mixed adds, 8M+2S, of
+//                     gathered affine bases, negated for negative digits, with
+//                     a one-ahead gather prefetch): perfect lane balance
+//                     whatever the bucket-size distribution.  Runs wholly
+//                     inside a segment go straight to their bucket; runs that
+//                     cross a segment edge leave a partial in a 2-slot record.
 //                     The dominant kernel: VALU-bound on v_mad_u64_u32.
-//  5. msm_reduce      per window, 2^(c-1)/LS segments of LS buckets: running
+//  5. msm_fixup       one thread per bucket: empty -> identity, shared ->
+//                     sum of its segment partials.
+//  6. msm_reduce      per window, 2^(c-1)/LS segments of LS buckets: running
 //                     sums (summation by parts, multiexp.cl:121-131) plus a
 //                     small-scalar multiple of the segment total.
-//  6. msm_sum         tree-fold of segment partials per window.
-//  7. msm_final       Horner fold over windows (c doublings each, as the
-//                     reference's host fold multiexp.rs:221-233), accumulate
-//                     across chunks, normalise to affine -> Jacobian (x, y, 1).
+//  7. msm_sum         tree-fold of segment partials to one sum per window.
+//  8. host fold       Horner over windows (c doublings each) and the final
+//                     affine normalisation on the host -- the reference GPU
+//                     path's own split (multiexp.rs:221-233): a serial chain of
+//                     ~256 doublings is ~25x faster on one CPU core than on one
+//                     GPU lane (host_field.hpp).
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <cstring>
+#include <vector>
 
 #include "ctx.hpp"
 #include "curve.hpp"
+#include "host_field.hpp"
 
 namespace ecg {
 
 constexpr int MSM_THREADS = 256;
-constexpr uint32_t MSM_SEG = 16;         // buckets per reduction segment
+constexpr uint32_t MSM_SEG = 32;         // buckets per reduction segment
+constexpr uint32_t MSM_ACC_SEG = 64;     // sorted entries per accumulation thread
 constexpr uint32_t MSM_FOLD = 32;        // fan-in of the partial-sum tree
 constexpr size_t MSM_MAX_CHUNK = 1ull << 27;  // terms per device pass
 
@@ -54,7 +67,9 @@ static MsmPlan make_plan(size_t n, uint32_t nbits) {
   for (uint32_t c = 2; c <= 22; c++) {
     uint32_t W = (nbits + 1 + c - 1) / c;
     double B = (double)(1u << (c - 1));
-    double cost = (double)n * W + W * B * 2.8 + W * c * 12.0;
+    // ~3.5 mixed-add equivalents per bucket in the reduction (2 full adds +
+    // the amortised segment scalar multiple), 1 per term per window.
+    double cost = (double)n * W + W * B * 4.0 + W * c * 12.0;
     if (cost < best) {
       best = cost;
       pl.c = c;
@@ -137,24 +152,86 @@ __global__ void __launch_bounds__(MSM_THREADS)
 }
 
 // ---------------------------------------------------------------------------
-// 4. bucket accumulation (dominant kernel)
+// 4. bucket accumulation over fixed-length segments (dominant kernel)
+// ---------------------------------------------------------------------------
+// Thread t owns sorted entries [t*SEG, (t+1)*SEG).  A run of bucket b is
+// "owned" when the whole bucket lies in one segment (start[b]/SEG ==
+// (end[b]-1)/SEG): its sum is final.  Otherwise the partial goes to record
+// slot 2t (b is the segment's first key) or 2t+1 (b is its last key).
+template <class C>
+ECG_DEV void acc_flush(uint32_t b, uint32_t first_key, const XYZZ<typename C::Fq>& acc, const uint32_t* start,
+                       const uint32_t* end, size_t t, XYZZ<typename C::Fq>* buckets, XYZZ<typename C::Fq>* recs) {
+  const uint32_t s0 = start[b], s1 = end[b];
+  if (s0 / MSM_ACC_SEG == (s1 - 1) / MSM_ACC_SEG) {
+    store_xyzz(&buckets[b], acc);
+  } else {
+    store_xyzz(&recs[2 * t + (b == first_key ? 0 : 1)], acc);
+  }
+}
+
+template <class C>
+__global__ void __launch_bounds__(MSM_THREADS)
+    msm_accumulate_kernel(const typename C::Fq* __restrict__ bases, const uint32_t* __restrict__ keys,
+                          const uint32_t* __restrict__ vals, size_t total, uint32_t sentinel,
+                          const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
+                          XYZZ<typename C::Fq>* __restrict__ buckets, XYZZ<typename C::Fq>* __restrict__ recs) {
+  using F = typename C::Fq;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t e0 = t * MSM_ACC_SEG;
+  if (e0 >= total) return;
+  const size_t e1 = e0 + MSM_ACC_SEG < total ? e0 + MSM_ACC_SEG : total;
+  const uint32_t first_key = keys[e0];
+  if (first_key >= sentinel) return;
+  uint32_t b = first_key;
+  uint32_t v = vals[e0];
+  Affine<F> P = load_affine(bases + 2 * (size_t)(v & 0x7fffffffu));
+  XYZZ<F> acc = xyzz_zero<F>();
+  for (size_t e = e0; e < e1; e++) {
+    // one-ahead prefetch of the next entry and its base
+    const bool more = e + 1 < e1;
+    const uint32_t kn = more ? keys[e + 1] : sentinel;
+    const uint32_t vn = more ? vals[e + 1] : 0u;
+    Affine<F> Pn;
+    if (kn < sentinel) Pn = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
+    if (!aff_is_identity(P)) {  // GpuRepr identity (impls.rs:52-54) contributes nothing
+      F ny = fneg(P.y);
+      if (v >> 31) P.y = ny;
+      acc = xyzz_add_affine(acc, P);
+    }
+    if (kn != b) {
+      acc_flush<C>(b, first_key, acc, start, end, t, buckets, recs);
+      if (kn >= sentinel) return;
+      acc = xyzz_zero<F>();
+      b = kn;
+    }
+    P = Pn;
+    v = vn;
+  }
+  acc_flush<C>(b, first_key, acc, start, end, t, buckets, recs);
+}
+
+// ---------------------------------------------------------------------------
+// 5. bucket fix-up: empty -> identity; shared -> sum of segment partials
 // ---------------------------------------------------------------------------
 template <class C>
 __global__ void __launch_bounds__(MSM_THREADS)
-    msm_accumulate_kernel(const typename C::Fq* __restrict__ bases, const uint32_t* __restrict__ vals,
-                          const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
-                          uint32_t nbuckets, XYZZ<typename C::Fq>* __restrict__ buckets) {
+    msm_fixup_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ start,
+                     const uint32_t* __restrict__ end, uint32_t nbuckets, const XYZZ<typename C::Fq>* __restrict__ recs,
+                     XYZZ<typename C::Fq>* __restrict__ buckets) {
   using F = typename C::Fq;
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nbuckets) return;
-  const uint32_t e0 = start[b], e1 = end[b];
+  const uint32_t s0 = start[b], s1 = end[b];
+  if (s1 == s0) {
+    store_xyzz(&buckets[b], xyzz_zero<F>());
+    return;
+  }
+  const uint32_t t0 = s0 / MSM_ACC_SEG, t1 = (s1 - 1) / MSM_ACC_SEG;
+  if (t0 == t1) return;  // written by msm_accumulate
   XYZZ<F> acc = xyzz_zero<F>();
-  for (uint32_t e = e0; e < e1; e++) {
-    const uint32_t v = vals[e];
-    Affine<F> P = load_affine(bases + 2 * (size_t)(v & 0x7fffffffu));
-    if (aff_is_identity(P)) continue;  // GpuRepr identity (impls.rs:52-54)
-    if (v >> 31) P.y = fneg(P.y);
-    acc = xyzz_add_affine(acc, P);
+  for (uint32_t t = t0; t <= t1; t++) {
+    const uint32_t slot = keys[(size_t)t * MSM_ACC_SEG] == b ? 0 : 1;
+    acc = xyzz_add(acc, load_xyzz(&recs[2 * (size_t)t + slot]));
   }
   store_xyzz(&buckets[b], acc);
 }
@@ -196,66 +273,6 @@ __global__ void __launch_bounds__(MSM_THREADS)
   XYZZ<F> acc = xyzz_zero<F>();
   for (uint32_t j = j0; j < j1; j++) acc = xyzz_add(acc, load_xyzz(&in[(size_t)w * cnt + j]));
   store_xyzz(&out[id], acc);
-}
-
-// ---------------------------------------------------------------------------
-// 7. Horner fold over windows; acc_io accumulates across chunks.
-// ---------------------------------------------------------------------------
-template <class C>
-__global__ void msm_final_kernel(const XYZZ<typename C::Fq>* __restrict__ win, MsmPlan pl,
-                                 XYZZ<typename C::Fq>* __restrict__ acc_io, int first) {
-  using F = typename C::Fq;
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  XYZZ<F> acc = xyzz_zero<F>();
-  for (int w = (int)pl.W - 1; w >= 0; w--) {
-    for (uint32_t k = 0; k < pl.c && !xyzz_is_zero(acc); k++) acc = xyzz_dbl(acc);
-    acc = xyzz_add(acc, load_xyzz(&win[w]));
-  }
-  if (!first) acc = xyzz_add(acc, load_xyzz(acc_io));
-  store_xyzz(acc_io, acc);
-}
-
-// XYZZ -> normalised Jacobian (x, y, 1) / (0, 1, 0), Montgomery limbs.
-template <class C>
-__global__ void msm_normalize_kernel(const XYZZ<typename C::Fq>* __restrict__ acc,
-                                     typename C::Fq* __restrict__ out_jac) {
-  using F = typename C::Fq;
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  XYZZ<F> p = load_xyzz(acc);
-  const bool inf = xyzz_is_zero(p);
-  Affine<F> a = xyzz_to_affine(p);
-  Jac<F> j = jac_from_affine_norm(a, inf);
-  store(&out_jac[0], j.X);
-  store(&out_jac[1], j.Y);
-  store(&out_jac[2], j.Z);
-}
-
-// Sum of `count` Jacobian points (ecg_point_sum_dev): block-strided partial
-// sums in one workgroup, then lane 0 folds them.
-template <class C>
-__global__ void __launch_bounds__(64)
-    point_sum_kernel(const typename C::Fq* __restrict__ pts, size_t count, XYZZ<typename C::Fq>* __restrict__ tmp,
-                     typename C::Fq* __restrict__ out_jac) {
-  using F = typename C::Fq;
-  const uint32_t t = threadIdx.x;
-  XYZZ<F> acc = xyzz_zero<F>();
-  for (size_t i = t; i < count; i += 64) {
-    Jac<F> j;
-    j.X = load(&pts[3 * i]);
-    j.Y = load(&pts[3 * i + 1]);
-    j.Z = load(&pts[3 * i + 2]);
-    acc = xyzz_add(acc, xyzz_from_jac(j));
-  }
-  store_xyzz(&tmp[t], acc);
-  __syncthreads();
-  if (t != 0) return;
-  __threadfence_block();
-  for (int k = 1; k < 64; k++) acc = xyzz_add(acc, load_xyzz(&tmp[k]));
-  const bool inf = xyzz_is_zero(acc);
-  Jac<F> r = jac_from_affine_norm(xyzz_to_affine(acc), inf);
-  store(&out_jac[0], r.X);
-  store(&out_jac[1], r.Y);
-  store(&out_jac[2], r.Z);
 }
 
 // ---------------------------------------------------------------------------
@@ -340,18 +357,15 @@ __global__ void __launch_bounds__(MSM_THREADS)
 static inline uint32_t blocks_for(size_t n, int threads) { return (uint32_t)((n + threads - 1) / threads); }
 
 template <class C>
-static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, void* d_out_jac,
+static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
                      hipStream_t s, ecg_abort_cb abort_cb, void* user) {
   using F = typename C::Fq;
   using X = XYZZ<F>;
-  void* accp;
-  ECG_TRY(ws_get(ctx, "msm_acc", sizeof(X), &accp));
-  X* acc = (X*)accp;
+  using HP = typename C::FqParams;
+  using HX = host::HXYZZ<HP>;
   kt_reset(ctx, "msm_accumulate");
-  if (n == 0) {
-    ECG_HIP(hipMemsetAsync(acc, 0, sizeof(X), s));  // ZZ = 0 -> identity
-  }
-  int first = 1;
+  HX total_acc = HX::zero();
+  std::vector<X> win;
   for (size_t off = 0; off < n; off += MSM_MAX_CHUNK) {
     if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144
     const size_t m = n - off < MSM_MAX_CHUNK ? n - off : MSM_MAX_CHUNK;
@@ -361,8 +375,9 @@ static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, s
     const uint32_t sentinel = nb;
     int key_bits = 1;
     while ((1ull << key_bits) <= sentinel) key_bits++;
+    const size_t nseg = (total + MSM_ACC_SEG - 1) / MSM_ACC_SEG;
 
-    void *k0, *k1, *v0, *v1, *st, *en, *bk, *pa, *pb, *tmp;
+    void *k0, *k1, *v0, *v1, *st, *en, *bk, *rc, *pa, *pb, *tmp;
     ECG_TRY(ws_get(ctx, "msm_k0", total * 4, &k0));
     ECG_TRY(ws_get(ctx, "msm_k1", total * 4, &k1));
     ECG_TRY(ws_get(ctx, "msm_v0", total * 4, &v0));
@@ -370,6 +385,7 @@ static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, s
     ECG_TRY(ws_get(ctx, "msm_start", (size_t)nb * 4, &st));
     ECG_TRY(ws_get(ctx, "msm_end", (size_t)nb * 4, &en));
     ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nb * sizeof(X), &bk));
+    ECG_TRY(ws_get(ctx, "msm_recs", 2 * nseg * sizeof(X), &rc));
     ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.W * pl.T * sizeof(X), &pa));
     ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.W * pl.T / MSM_FOLD + pl.W) * sizeof(X), &pb));
 
@@ -394,10 +410,15 @@ static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, s
     ECG_HIP(hipGetLastError());
 
     ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
-    hipLaunchKernelGGL(msm_accumulate_kernel<C>, dim3(blocks_for(nb, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                       bases, (const uint32_t*)v1, (const uint32_t*)st, (const uint32_t*)en, nb, (X*)bk);
+    hipLaunchKernelGGL(msm_accumulate_kernel<C>, dim3(blocks_for(nseg, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                       bases, (const uint32_t*)k1, (const uint32_t*)v1, total, sentinel, (const uint32_t*)st,
+                       (const uint32_t*)en, (X*)bk, (X*)rc);
     ECG_HIP(hipGetLastError());
     ECG_TRY(kt_end(ctx, "msm_accumulate", s));
+
+    hipLaunchKernelGGL(msm_fixup_kernel<C>, dim3(blocks_for(nb, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                       (const uint32_t*)k1, (const uint32_t*)st, (const uint32_t*)en, nb, (const X*)rc, (X*)bk);
+    ECG_HIP(hipGetLastError());
 
     hipLaunchKernelGGL(msm_reduce_kernel<C>, dim3(blocks_for((size_t)pl.W * pl.T, MSM_THREADS)),
                        dim3(MSM_THREADS), 0, s, (const X*)bk, pl, (X*)pa);
@@ -416,24 +437,35 @@ static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, s
       out = t;
       cnt = oc;
     }
-    hipLaunchKernelGGL(msm_final_kernel<C>, dim3(1), dim3(64), 0, s, (const X*)in, pl, acc, first);
-    ECG_HIP(hipGetLastError());
-    first = 0;
+    // window sums -> host; Horner fold over windows (multiexp.rs:221-233)
+    win.resize(pl.W);
+    ECG_HIP(hipMemcpyAsync(win.data(), in, pl.W * sizeof(X), hipMemcpyDeviceToHost, s));
+    ECG_HIP(hipStreamSynchronize(s));
+    HX acc = HX::zero();
+    for (int w = (int)pl.W - 1; w >= 0; w--) {
+      for (uint32_t k = 0; k < pl.c; k++) acc = host::hdbl(acc);
+      HX ww;
+      memcpy(ww.X.v, win[w].X.v, sizeof(ww.X.v));
+      memcpy(ww.Y.v, win[w].Y.v, sizeof(ww.Y.v));
+      memcpy(ww.ZZ.v, win[w].ZZ.v, sizeof(ww.ZZ.v));
+      memcpy(ww.ZZZ.v, win[w].ZZZ.v, sizeof(ww.ZZZ.v));
+      acc = host::hadd_pts(acc, ww);
+    }
+    total_acc = host::hadd_pts(total_acc, acc);
   }
-  hipLaunchKernelGGL(msm_normalize_kernel<C>, dim3(1), dim3(64), 0, s, (const X*)acc, (F*)d_out_jac);
-  ECG_HIP(hipGetLastError());
+  host::hto_jac_norm(total_acc, out_jac);
   return ECG_OK;
 }
 
-int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, void* d_out_jac,
+int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
             hipStream_t s, ecg_abort_cb abort_cb, void* user) {
   if (n > 0x7fffffffull) {
     set_error("multiexp: at most 2^31-1 terms per call");
     return ECG_ERR_INVALID;
   }
   switch (curve_id) {
-    case ECG_CURVE_BLS12_381: return msm_run_t<BLS12_381>(ctx, d_bases, d_scalars, n, d_out_jac, s, abort_cb, user);
-    case ECG_CURVE_BN254: return msm_run_t<BN254>(ctx, d_bases, d_scalars, n, d_out_jac, s, abort_cb, user);
+    case ECG_CURVE_BLS12_381: return msm_run_t<BLS12_381>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user);
+    case ECG_CURVE_BN254: return msm_run_t<BN254>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user);
     default:
       set_error("multiexp: unknown curve_id %d", curve_id);
       return ECG_ERR_INVALID;
@@ -441,24 +473,34 @@ int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scala
 }
 
 template <class C>
-static int point_sum_t(ecg_ctx* ctx, const void* d_points, size_t count, void* d_out, hipStream_t s) {
-  using X = XYZZ<typename C::Fq>;
-  void* tmp;
-  ECG_TRY(ws_get(ctx, "psum_tmp", 64 * sizeof(X), &tmp));
-  hipLaunchKernelGGL(point_sum_kernel<C>, dim3(1), dim3(64), 0, s, (const typename C::Fq*)d_points, count, (X*)tmp,
-                     (typename C::Fq*)d_out);
-  ECG_HIP(hipGetLastError());
-  return ECG_OK;
+static void point_sum_host_t(const uint64_t* pts, size_t count, uint64_t* out_jac) {
+  using HP = typename C::FqParams;
+  constexpr int N = HP::N;
+  host::HXYZZ<HP> acc = host::HXYZZ<HP>::zero();
+  for (size_t i = 0; i < count; i++) acc = host::hadd_pts(acc, host::hfrom_jac<HP>(&pts[i * 3 * N]));
+  host::hto_jac_norm(acc, out_jac);
 }
 
-int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, void* d_out_jac, hipStream_t s) {
+int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac) {
   switch (curve_id) {
-    case ECG_CURVE_BLS12_381: return point_sum_t<BLS12_381>(ctx, d_points, count, d_out_jac, s);
-    case ECG_CURVE_BN254: return point_sum_t<BN254>(ctx, d_points, count, d_out_jac, s);
+    case ECG_CURVE_BLS12_381: point_sum_host_t<BLS12_381>(points, count, out_jac); return ECG_OK;
+    case ECG_CURVE_BN254: point_sum_host_t<BN254>(points, count, out_jac); return ECG_OK;
     default:
       set_error("point_sum: unknown curve_id %d", curve_id);
       return ECG_ERR_INVALID;
   }
+}
+
+int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, uint64_t* out_jac, hipStream_t s) {
+  if (curve_id != ECG_CURVE_BLS12_381 && curve_id != ECG_CURVE_BN254) {
+    set_error("point_sum: unknown curve_id %d", curve_id);
+    return ECG_ERR_INVALID;
+  }
+  std::vector<uint64_t> pts(count * 3 * (size_t)fq_limbs64(curve_id));
+  if (count) ECG_HIP(hipMemcpyAsync(pts.data(), d_points, pts.size() * 8, hipMemcpyDeviceToHost, s));
+  ECG_HIP(hipStreamSynchronize(s));
+  (void)ctx;
+  return point_sum_host(curve_id, pts.data(), count, out_jac);
 }
 
 template <class C>

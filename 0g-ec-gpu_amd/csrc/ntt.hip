@@ -242,6 +242,26 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
   return ECG_OK;
 }
 
+int ntt_validate(int field_id, uint32_t log_n) {
+  uint32_t adic;
+  switch (field_id) {
+    case ECG_FIELD_BLS12_381_FR: adic = params::bls12_381_fr::TWO_ADICITY; break;
+    case ECG_FIELD_BN254_FR: adic = params::bn254_fr::TWO_ADICITY; break;
+    default:
+      set_error("radix_fft: field_id %d is not an FFT-friendly scalar field", field_id);
+      return ECG_ERR_INVALID;
+  }
+  if (log_n == 0) {
+    set_error("radix_fft: log_n must be >= 1");  // the reference panics (fft.rs:68-70)
+    return ECG_ERR_INVALID;
+  }
+  if (log_n > adic || log_n > 32) {
+    set_error("radix_fft: log_n %u exceeds the field's two-adicity %u", log_n, adic);
+    return ECG_ERR_INVALID;
+  }
+  return ECG_OK;
+}
+
 int ntt_run(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uint32_t log_n, hipStream_t s,
             ecg_abort_cb abort_cb, void* user) {
   switch (field_id) {

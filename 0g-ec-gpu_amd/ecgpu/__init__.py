@@ -85,11 +85,16 @@ _SIGS = {
                                    ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "ecg_point_sum_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, _u64p,
                                          ctypes.c_void_p]),
+    "ecg_point_sum": (ctypes.c_int, [ctypes.c_int, _u64p, ctypes.c_size_t, _u64p]),
     "ecg_msm_check_bases": (ctypes.c_int, [ctypes.c_int, _u64p, _u64p, ctypes.c_size_t]),
     "ecg_gen_bases_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, ctypes.c_size_t,
                                          ctypes.c_void_p, ctypes.c_void_p]),
     "ecg_last_kernel_time": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_int)]),
+    "ecg_dev_alloc": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    "ecg_dev_free": (None, [ctypes.c_void_p, ctypes.c_void_p]),
+    "ecg_dev_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "ecg_dev_download": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
 }
 
 
@@ -268,6 +273,75 @@ class Program:
             self.close()
         except Exception:
             pass
+
+
+class DeviceBuffer:
+    """HBM-resident buffer on a Program's device (DeviceData / upload_multiexp_bases
+    analogue).  `ptr` feeds the device-resident entry points."""
+
+    def __init__(self, prog: Program, nbytes: int):
+        self.program = prog
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        _check(lib().ecg_dev_alloc(prog.handle, self.nbytes, ctypes.byref(p)), "dev_alloc")
+        self.ptr = p
+
+    @staticmethod
+    def upload(prog: Program, host: np.ndarray) -> "DeviceBuffer":
+        h = np.ascontiguousarray(host)
+        buf = DeviceBuffer(prog, h.nbytes)
+        buf.write(h)
+        return buf
+
+    def write(self, host: np.ndarray) -> None:
+        h = np.ascontiguousarray(host)
+        if h.nbytes > self.nbytes:
+            raise EcError("DeviceBuffer.write: host array larger than the buffer")
+        _check(lib().ecg_dev_upload(self.program.handle, self.ptr, h.ctypes.data_as(ctypes.c_void_p), h.nbytes))
+
+    def read(self, dtype=np.uint64, shape=None) -> np.ndarray:
+        out = np.empty(self.nbytes // np.dtype(dtype).itemsize, dtype=dtype)
+        _check(lib().ecg_dev_download(self.program.handle, out.ctypes.data_as(ctypes.c_void_p), self.ptr,
+                                      out.nbytes))
+        return out.reshape(shape) if shape is not None else out
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().ecg_dev_free(self.program.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "program", None) is not None and self.program.handle:
+                self.free()
+        except Exception:
+            pass
+
+
+def msm_dev(prog: Program, curve, d_bases: DeviceBuffer, d_scalars: DeviceBuffer, n: int) -> np.ndarray:
+    """MSM over HBM-resident bases/scalars (ecg_msm_dev) -> Jacobian (3*Lq,)."""
+    cid = _curve(curve)
+    out = np.zeros(3 * CURVE_FQ_LIMBS[cid], dtype=np.uint64)
+    _check(lib().ecg_msm_dev(prog.handle, cid, d_bases.ptr, d_scalars.ptr, n,
+                             out.ctypes.data_as(ctypes.c_void_p), 0, None), "msm_dev")
+    return out
+
+
+def fft_dev(prog: Program, field, d_data: DeviceBuffer, omega: np.ndarray, log_n: int) -> None:
+    """In-place NTT of HBM-resident data (ecg_fft_dev)."""
+    fid = _fft_field(field)
+    om = np.ascontiguousarray(omega, dtype=np.uint64).reshape(4)
+    _check(lib().ecg_fft_dev(prog.handle, fid, d_data.ptr, _ptr(om), log_n, None), "fft_dev")
+
+
+def gen_bases_dev(prog: Program, curve, a: int, b: int, n: int) -> DeviceBuffer:
+    """Synthetic bases P_i = (a + i b) G generated on the device."""
+    cid = _curve(curve)
+    buf = DeviceBuffer(prog, n * 2 * CURVE_FQ_LIMBS[cid] * 8)
+    au = np.array([(a >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+    bu = np.array([(b >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+    _check(lib().ecg_gen_bases_dev(prog.handle, cid, _ptr(au), _ptr(bu), n, buf.ptr, None), "gen_bases")
+    return buf
 
 
 def program(device: Device) -> Program:

@@ -123,11 +123,23 @@ int ecg_msm_dev(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_s
  * per-GPU partials (RCCL has no EC-add reduction op).  out is host memory. */
 int ecg_point_sum_dev(ecg_ctx *ctx, int curve_id, const void *d_points, size_t count,
                       uint64_t *out_jac, void *stream);
+/* Same fold over host memory (multiexp.rs:394-397 cross-device sum). */
+int ecg_point_sum(int curve_id, const uint64_t *points, size_t count, uint64_t *out_jac);
 
 /* Returns ECG_ERR_INVALID with "Encountered an identity element in the
  * CRS." if any base with a non-zero scalar is the identity -- the
  * reference CPU path's error behaviour (multiexp_cpu.rs:57-61). */
 int ecg_msm_check_bases(int curve_id, const uint64_t *bases_xy, const uint64_t *scalars, size_t n);
+
+/* ---- device buffers on ctx's device ---------------------------------------
+ * Keep bases / polynomials resident in HBM across calls: the analogue of
+ * ag_cuda_ec::multiexp::upload_multiexp_bases and ag-cuda-proxy's
+ * DeviceData::upload (ag-cuda-ec/src/multiexp.rs:11-19,
+ * ag-cuda-proxy/src/params.rs:112-219).  Pointers feed the *_dev calls. */
+int ecg_dev_alloc(ecg_ctx *ctx, size_t bytes, void **out);
+void ecg_dev_free(ecg_ctx *ctx, void *d_ptr);
+int ecg_dev_upload(ecg_ctx *ctx, void *d_dst, const void *src, size_t bytes);
+int ecg_dev_download(ecg_ctx *ctx, void *dst, const void *d_src, size_t bytes);
 
 /* ---- synthetic inputs for benchmarks/tests (not part of the reference API)
  * Bases P_i = (a + i*b) * G for i < n written to device memory d_out

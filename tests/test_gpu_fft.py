@@ -1,0 +1,160 @@
+"""GPU parity tests of the HIP NTT through the C ABI (FftKernel mirror).
+
+Model: ec-gpu-proxy/tests/fft.rs (gpu_fft_consistency, log_d 1..=16;
+gpu_fft_many_consistency, 3 transforms per call, log_d 1..=20), compared
+bit-exactly against the CPU oracle's serial_fft / parallel_fft and against the
+committed golden fixtures.  Full-size (2^24) parity is in bench.py and
+test_fft_2p24_matches_parallel_fft below."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import coracle as co
+import ecgpu
+import py_oracle as po
+from conftest import GOLDEN, load_npz
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = [("bls12_381_fr", 0), ("bn254_fr", 2)]
+
+
+def rand_mont(f, n, seed):
+    rng = np.random.default_rng(seed)
+    # uniform limbs reduced below r: any value < r is a valid Montgomery form
+    a = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+    a[:, 3] &= np.uint64((1 << (f.bits - 192 - 1)) - 1)  # < 2^(bits-1) < r
+    return a
+
+
+@pytest.fixture(scope="module")
+def kernels(gpu_programs):
+    progs, _ = gpu_programs
+    return {name: ecgpu.FftKernel.create(progs, name) for name, _ in FIELDS}
+
+
+@pytest.mark.parametrize("fname,fid", FIELDS)
+def test_fft_golden(kernels, fname, fid):
+    g = load_npz(f"fft_{fname}.npz")
+    for log_n in range(1, 11):
+        a = g[f"in_{log_n}"].copy()
+        kernels[fname].radix_fft(a, g[f"omega_{log_n}"], log_n)
+        assert (a == g[f"out_{log_n}"]).all(), log_n
+
+
+def test_config1_fft_2p16_hash(kernels):
+    """BASELINE config (1) input run through the GPU path reproduces the
+    serial_fft fixture hash."""
+    meta = json.load(open(os.path.join(GOLDEN, "fft_bls12_381_fr_2p16.json")))
+    f = po.BLS12_381_FR
+    n = 1 << 16
+    rng = po.Xoshiro256ss(0x0FF70016)
+    a = co.u64arr([f.to_mont(rng.field_element(f)) for _ in range(n)], 4)
+    assert hashlib.sha256(a.tobytes()).hexdigest() == meta["input_sha256"]
+    kernels["bls12_381_fr"].radix_fft(a, co.u64arr([f.to_mont(f.omega(n))], 4)[0], 16)
+    assert hashlib.sha256(a.tobytes()).hexdigest() == meta["output_sha256"]
+
+
+@pytest.mark.parametrize("fname,fid", FIELDS)
+def test_gpu_fft_consistency(kernels, fname, fid):
+    """tests/fft.rs gpu_fft_consistency: log_d 1..=16 (plus 17..20), GPU == CPU."""
+    f = po.FIELDS[fname]
+    for log_d in range(1, 21):
+        n = 1 << log_d
+        a = rand_mont(f, n, 1000 + log_d)
+        om = co.u64arr([f.to_mont(f.omega(n))], 4)[0]
+        ref = co.serial_fft(fid, a, om, log_d) if log_d <= 12 else co.parallel_fft(fid, a, om, log_d, 3)
+        g = a.copy()
+        kernels[fname].radix_fft_many([g], [om], [log_d])
+        assert (g == ref).all(), log_d
+
+
+def test_gpu_fft_many_consistency(kernels):
+    """tests/fft.rs gpu_fft_many_consistency: 3 transforms per call."""
+    f = po.BLS12_381_FR
+    for log_d in (1, 5, 9, 13, 17):
+        n = 1 << log_d
+        ins = [rand_mont(f, n, 7 * log_d + j) for j in range(3)]
+        om = co.u64arr([f.to_mont(f.omega(n))], 4)[0]
+        refs = [co.serial_fft(0, a, om, log_d) if log_d <= 12 else co.parallel_fft(0, a, om, log_d, 2) for a in ins]
+        outs = [a.copy() for a in ins]
+        kernels["bls12_381_fr"].radix_fft_many(outs, [om] * 3, [log_d] * 3)
+        for o, r in zip(outs, refs):
+            assert (o == r).all(), log_d
+
+
+def test_fft_many_mixed_sizes_and_omegas(kernels):
+    f = po.BLS12_381_FR
+    sizes = [3, 11, 8, 14]
+    ins = [rand_mont(f, 1 << s, s) for s in sizes]
+    oms = [co.u64arr([f.to_mont(pow(f.omega(1 << s), 3, f.modulus))], 4)[0] for s in sizes]  # other generators
+    refs = [co.serial_fft(0, a, om, s) for a, om, s in zip(ins, oms, sizes)]
+    outs = [a.copy() for a in ins]
+    kernels["bls12_381_fr"].radix_fft_many(outs, oms, sizes)
+    for o, r in zip(outs, refs):
+        assert (o == r).all()
+
+
+def test_fft_edge_values(kernels):
+    f = po.BLS12_381_FR
+    n = 1 << 9
+    om = co.u64arr([f.to_mont(f.omega(n))], 4)[0]
+    for vals in ([0] * n, [f.modulus - 1] * n, [1] + [0] * (n - 1)):
+        a = co.u64arr([f.to_mont(v) for v in vals], 4)
+        ref = co.serial_fft(0, a, om, 9)
+        kernels["bls12_381_fr"].radix_fft(a, om, 9)
+        assert (a == ref).all()
+
+
+def test_inverse_round_trip_2p22(kernels):
+    """Size-independent property at 2^22: FFT(omega^-1) o FFT(omega) = n * id."""
+    f = po.BLS12_381_FR
+    log_n = 22
+    n = 1 << log_n
+    a = rand_mont(f, n, 22)
+    w = f.omega(n)
+    om = co.u64arr([f.to_mont(w)], 4)[0]
+    om_inv = co.u64arr([f.to_mont(pow(w, -1, f.modulus))], 4)[0]
+    b = a.copy()
+    k = kernels["bls12_381_fr"]
+    k.radix_fft(b, om, log_n)
+    k.radix_fft(b, om_inv, log_n)
+    # compare b == n * a on a sample of rows (exact field arithmetic)
+    idx = np.random.default_rng(0).integers(0, n, size=512)
+    for i in idx:
+        x = f.from_mont(co.to_ints(a[i:i + 1])[0])
+        y = f.from_mont(co.to_ints(b[i:i + 1])[0])
+        assert y == x * n % f.modulus
+
+
+def test_fft_2p24_matches_parallel_fft(kernels):
+    """BASELINE config (2): Fr NTT 2^24 on one MI355X, bit-exact vs CPU parallel_fft."""
+    f = po.BLS12_381_FR
+    log_n = 24
+    a = rand_mont(f, 1 << log_n, 24)
+    om = co.u64arr([f.to_mont(f.omega(1 << log_n))], 4)[0]
+    ref = co.parallel_fft(0, a, om, log_n, 4)
+    kernels["bls12_381_fr"].radix_fft(a, om, log_n)
+    assert (a == ref).all()
+
+
+def test_fft_errors_and_abort(kernels, gpu_programs):
+    f = po.BLS12_381_FR
+    k = kernels["bls12_381_fr"]
+    om = co.u64arr([f.to_mont(1)], 4)[0]
+    with pytest.raises(ecgpu.EcError, match="log_n"):          # reference panics at log_n = 0
+        k.radix_fft(np.zeros((1, 4), np.uint64), om, 0)
+    progs, _ = gpu_programs
+    small = np.zeros((2, 4), np.uint64)
+    rc = ecgpu.lib().ecg_fft(progs[0].handle, ecgpu.FIELD_BN254_FR, ecgpu._ptr(small), ecgpu._ptr(om), 29,
+                             ecgpu.ABORT_CB(0), None)
+    assert rc == ecgpu.ECG_ERR_INVALID and "two-adicity" in ecgpu.last_error()  # BN254 Fr: 2-adicity 28
+    rc = ecgpu.lib().ecg_fft(progs[0].handle, ecgpu.FIELD_BLS12_381_FQ, ecgpu._ptr(small), ecgpu._ptr(om), 1,
+                             ecgpu.ABORT_CB(0), None)
+    assert rc == ecgpu.ECG_ERR_INVALID
+    ka = ecgpu.FftKernel.create_with_abort(progs, lambda: True)
+    with pytest.raises(ecgpu.Aborted):
+        ka.radix_fft(np.zeros((16, 4), np.uint64), om, 4)

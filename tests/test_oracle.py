@@ -1,0 +1,174 @@
+"""CPU tests: pin the oracle (C restatement + Python restatement) before it is
+trusted as the checker for the HIP path.
+
+Pinning sources: the reference holds no golden vectors and cannot
+be built here, so the oracle is pinned by (1) public curve constants,
+(2) the reference's own property tests restated (multiexp_cpu.rs test_with_bls12,
+fft_cpu.rs parallel_fft_consistency), (3) agreement of two independent
+restatements (C limbs vs Python big ints) through the committed fixtures.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import coracle as co
+import py_oracle as po
+from conftest import GOLDEN, load_npz
+
+
+# ---------------------------------------------------------------- constants
+def test_public_constants():
+    # ark-bls12-381 Fq: R mod p and -p^-1 mod 2^64 (the well-known blst/zkcrypto values)
+    fq = po.BLS12_381_FQ
+    assert fq.R % fq.modulus == int(
+        "15f65ec3fa80e4935c071a97a256ec6d77ce5853705257455f48985753c758baebf4000bc40c0002760900000002fffd", 16)
+    assert (-pow(fq.modulus, -1, 1 << 64)) % (1 << 64) == 0x89F3FFFCFFFCFFFD
+    # two-adic roots of unity (FftField::TWO_ADIC_ROOT_OF_UNITY)
+    assert po.BLS12_381_FR.two_adic_root() == 0x16A2A19EDFE81F20D09B681922C813B4B63683508C2280B93829971F439F0D2B
+    assert po.BN254_FR.two_adic_root() == \
+        19103219067921713944291392827692070036145651957329286315305642004821462161904
+    for f in (po.BLS12_381_FR, po.BN254_FR):
+        w = f.two_adic_root()
+        assert pow(w, 1 << f.two_adicity, f.modulus) == 1
+        assert pow(w, 1 << (f.two_adicity - 1), f.modulus) == f.modulus - 1
+    for cv in (po.BLS12_381, po.BN254):
+        assert po.on_curve(cv, (cv.gx, cv.gy))
+
+
+@pytest.mark.parametrize("cid", [0, 1])
+def test_group_order(cid):
+    cv = po.CURVES[["bls12_381", "bn254"][cid]]
+    assert co.jac_to_affine(cid, co.gen_mul(cid, cv.fr.modulus)) is None          # r G = O
+    g1 = co.jac_to_affine(cid, co.gen_mul(cid, cv.fr.modulus + 1))                 # (r+1) G = G
+    assert co.to_ints(g1.reshape(2, -1)) == [cv.fq.to_mont(cv.gx), cv.fq.to_mont(cv.gy)]
+
+
+@pytest.mark.parametrize("fname", ["bls12_381_fr", "bls12_381_fq", "bn254_fr", "bn254_fq"])
+def test_field_mul_matches_bigint(fname):
+    f = po.FIELDS[fname]
+    fid = co.FIELD_IDS[fname]
+    rng = po.Xoshiro256ss(11)
+    xs = [rng.field_element(f) for _ in range(64)] + [0, 1, f.modulus - 1]
+    ys = [rng.field_element(f) for _ in range(64)] + [f.modulus - 1, f.modulus - 1, f.modulus - 1]
+    A = co.u64arr([f.to_mont(x) for x in xs], f.limbs64)
+    B = co.u64arr([f.to_mont(y) for y in ys], f.limbs64)
+    for k in range(len(xs)):
+        r = np.zeros(f.limbs64, np.uint64)
+        co.lib().orc_fmul(fid, co.ptr(r), co.ptr(A[k]), co.ptr(B[k]))
+        assert co.to_ints(r.reshape(1, -1))[0] == f.to_mont(xs[k] * ys[k])
+        co.lib().orc_fadd(fid, co.ptr(r), co.ptr(A[k]), co.ptr(B[k]))
+        assert co.to_ints(r.reshape(1, -1))[0] == f.to_mont(xs[k] + ys[k])
+        co.lib().orc_fsub(fid, co.ptr(r), co.ptr(A[k]), co.ptr(B[k]))
+        assert co.to_ints(r.reshape(1, -1))[0] == f.to_mont(xs[k] - ys[k])
+
+
+# ---------------------------------------------------------------- FFT
+@pytest.mark.parametrize("fname", ["bls12_381_fr", "bn254_fr"])
+def test_serial_fft_matches_golden(fname):
+    fid = co.FIELD_IDS[fname]
+    g = load_npz(f"fft_{fname}.npz")
+    for log_n in range(1, 11):
+        out = co.serial_fft(fid, g[f"in_{log_n}"], g[f"omega_{log_n}"], log_n)
+        assert (out == g[f"out_{log_n}"]).all(), log_n
+
+
+@pytest.mark.parametrize("fname", ["bls12_381_fr", "bn254_fr"])
+def test_parallel_fft_consistency(fname):
+    """fft_cpu.rs:127-167 parallel_fft_consistency (log_d 0..10, log_threads <= 2)."""
+    f = po.FIELDS[fname]
+    fid = co.FIELD_IDS[fname]
+    rng = po.Xoshiro256ss(5)
+    for log_d in range(0, 11):
+        d = 1 << log_d
+        a = co.u64arr([f.to_mont(rng.field_element(f)) for _ in range(d)], 4)
+        om = co.u64arr([f.to_mont(f.omega(d))], 4)[0]
+        ref = co.serial_fft(fid, a, om, log_d)
+        for lt in range(0, min(log_d, 3) + 1):
+            assert (co.parallel_fft(fid, a, om, log_d, lt) == ref).all(), (log_d, lt)
+
+
+def test_fft_known_answers():
+    f = po.BLS12_381_FR
+    log_n = 6
+    n = 1 << log_n
+    om = co.u64arr([f.to_mont(f.omega(n))], 4)[0]
+    delta = co.u64arr([f.to_mont(1)] + [0] * (n - 1), 4)
+    ones = co.u64arr([f.to_mont(1)] * n, 4)
+    assert (co.serial_fft(0, delta, om, log_n) == ones).all()           # DFT(delta_0) = 1
+    want = co.u64arr([f.to_mont(n)] + [0] * (n - 1), 4)
+    assert (co.serial_fft(0, ones, om, log_n) == want).all()            # DFT(1) = n delta_0
+
+
+def test_config1_serial_fft_2p16_hash():
+    """BASELINE config (1): BLS12-381 Fr FFT 2^16 on serial_fft -- C restatement
+    reproduces the Python restatement's output hash."""
+    meta = json.load(open(os.path.join(GOLDEN, "fft_bls12_381_fr_2p16.json")))
+    f = po.BLS12_381_FR
+    n = 1 << 16
+    rng = po.Xoshiro256ss(0x0FF70016)
+    a = co.u64arr([f.to_mont(rng.field_element(f)) for _ in range(n)], 4)
+    assert hashlib.sha256(a.tobytes()).hexdigest() == meta["input_sha256"]
+    om = co.u64arr([f.to_mont(f.omega(n))], 4)[0]
+    out = co.serial_fft(0, a, om, 16)
+    assert hashlib.sha256(out.tobytes()).hexdigest() == meta["output_sha256"]
+    assert (co.parallel_fft(0, a, om, 16, 3) == out).all()
+
+
+# ---------------------------------------------------------------- MSM
+@pytest.mark.parametrize("cname", ["bls12_381", "bn254"])
+def test_multiexp_cpu_matches_golden(cname):
+    cid = co.CURVE_IDS[cname]
+    g = load_npz(f"msm_{cname}.npz")
+    for k, n in enumerate(g["cases"]):
+        out = co.multiexp_cpu(cid, g[f"bases_{k}"], g[f"exps_{k}"], nthreads=4)
+        aff = co.jac_to_affine(cid, out)
+        if g[f"inf_{k}"][0]:
+            assert aff is None
+        else:
+            assert (aff == g[f"out_{k}"]).all(), n
+
+
+def test_multiexp_cpu_vs_naive_bls12():
+    """multiexp_cpu.rs:380-420 test_with_bls12 (naive == Pippenger), at 2^10."""
+    cid = 0
+    n = 1 << 10
+    rng = po.Xoshiro256ss(12)
+    B = co.gen_bases(cid, 99, 101, n, 4)
+    E = co.u64arr([rng.field_element(po.BLS12_381_FR) for _ in range(n)], 4)
+    fast = co.jac_to_affine(cid, co.multiexp_cpu(cid, B, E, nthreads=4))
+    naive = co.jac_to_affine(cid, co.naive_multiexp(cid, B, E))
+    assert (fast == naive).all()
+
+
+def test_multiexp_cpu_rejects_identity_base():
+    """multiexp_cpu.rs:57-61: 'Encountered an identity element in the CRS.'"""
+    g = load_npz("msm_bls12_381.npz")
+    B = g["bases_2"].copy()
+    E = g["exps_2"].copy()
+    B[1] = 0
+    E[1] = [5, 0, 0, 0]
+    with pytest.raises(co.IdentityBaseError):
+        co.multiexp_cpu(0, B, E)
+
+
+@pytest.mark.parametrize("cid", [0, 1])
+def test_kat_construction(cid):
+    """Bases P_i = (a + i b) G: sum s_i P_i == (sum s_i (a + i b) mod r) G."""
+    cv = po.CURVES[["bls12_381", "bn254"][cid]]
+    rng = po.Xoshiro256ss(77)
+    n = 300
+    a, b = 0xABCDEF, 0x123457
+    B = co.gen_bases(cid, a, b, n, 4)
+    E = co.u64arr([rng.field_element(cv.fr) for _ in range(n)], 4)
+    kat = co.kat_scalar(cid, a, b, E, nthreads=3)
+    assert kat == sum(int(e) * (a + i * b) for i, e in enumerate(co.to_ints(E))) % cv.fr.modulus
+    want = co.jac_to_affine(cid, co.gen_mul(cid, kat))
+    got = co.jac_to_affine(cid, co.multiexp_cpu(cid, B, E, nthreads=4))
+    assert (want == got).all()
+    # and the bases really are (a + i b) G
+    for i in (0, 1, n - 1):
+        pi = co.jac_to_affine(cid, co.gen_mul(cid, a + i * b))
+        assert (pi == B[i]).all()
