@@ -36,6 +36,19 @@ __global__ void k_chain(const F* x, const F* y, F* out, int n) {
   store(&out[t], r);
 }
 
+// Same chain, but one chain per thread and occupancy forced by dynamic LDS:
+// waves/SIMD = 8 / (blocks of 256 per CU limited by LDS).
+template <class F>
+__global__ void k_chain_occ(const F* x, const F* y, F* out, int n) {
+  extern __shared__ uint32_t lds_pad[];
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  F a = load(&x[t]), b = load(&y[t]);
+  for (int i = 0; i < ITERS; i++) a = fmul(a, b);
+  if (threadIdx.x == 1023) lds_pad[0] = a.v[0];  // keep the LDS allocation
+  store(&out[t], a);
+}
+
 template <class F>
 __global__ void k_once(const F* x, const F* y, F* o0, F* o1, int n) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -102,6 +115,20 @@ static void bench(const char* name, int fid, orc_fmul_t orc) {
     }
     double muls = (double)n * ITERS * CH;
     printf("  %-6s %s: %8.3f ms  %8.2f G mul/s\n", name, v == 0 ? "fips-asm-x1" : v == 1 ? "cios-c++" : "fips-asm-x4", best, muls / best / 1e6);
+  }
+  // throughput vs occupancy (1 chain per thread): LDS per 256-thread block sets blocks/CU
+  for (int wps : {1, 2, 3, 4, 8}) {
+    size_t lds = wps >= 8 ? 0 : (160 * 1024) / wps - 256;  // blocks per CU = wps (each block = 1 wave/SIMD)
+    float best = 1e30f;
+    for (int rep = 0; rep < 3; rep++) {
+      CHK(hipEventRecord(a));
+      hipLaunchKernelGGL(k_chain_occ<F>, dim3(n / 256), dim3(256), lds, 0, dx, dy, d0, n);
+      CHK(hipEventRecord(b));
+      CHK(hipEventSynchronize(b));
+      float ms; CHK(hipEventElapsedTime(&ms, a, b));
+      if (ms < best) best = ms;
+    }
+    printf("  %-6s occupancy %d wave(s)/SIMD: %8.2f G mul/s\n", name, wps, (double)n * ITERS / best / 1e6);
   }
   CHK(hipFree(dx)); CHK(hipFree(dy)); CHK(hipFree(d0)); CHK(hipFree(d1));
 }
