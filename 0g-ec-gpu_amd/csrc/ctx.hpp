@@ -56,6 +56,7 @@ struct ecg_ctx {
   std::map<std::string, Buf> ws;
   // FFT twiddle-table cache key
   int tw_fid = -1;
+  int tw_variant = 0;
   uint32_t tw_log_n = 0;
   uint64_t tw_omega[4] = {0, 0, 0, 0};
   // kernel timing (HIP events on the launch stream)

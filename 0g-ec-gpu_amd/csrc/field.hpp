@@ -93,28 +93,39 @@ ECG_DEV void mac96s(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b_uniform
       : "v"(a), "s"(b_uniform));
 }
 
-// r = a + b over L limbs; returns carry-out.
+// Montgomery digit m = lo * (-p^-1) mod 2^32.  v_mul_lo_u32 is quarter rate on
+// gfx950 (tools/mad_microbench.hip); the low half of a half-rate
+// v_mad_u64_u32 with a zero addend is the same value at half the cost.
+// (-p^-1 = 0xffffffff, BLS12-381 Fr: a plain negation.)
+template <class P>
+ECG_DEV uint32_t mont_digit(uint32_t lo) {
+  constexpr uint32_t inv = (uint32_t)P::INV;
+  if constexpr (inv == 0xffffffffu) {
+    return 0u - lo;
+  } else {
+    uint64_t r, cc;
+    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cc) : "v"(lo), "s"(inv));
+    return (uint32_t)r;
+  }
+}
+
+// r = a + b over L limbs; returns carry-out.  __builtin_addc/subc lower to
+// v_add_co_u32 / v_addc_co_u32 chains (one VALU op per limb).
 template <int L>
 ECG_DEV uint32_t add_limbs(uint32_t* r, const uint32_t* a, const uint32_t* b) {
-  uint64_t c = 0;
+  unsigned c = 0;
 #pragma unroll
-  for (int i = 0; i < L; i++) {
-    c = (uint64_t)a[i] + b[i] + (c >> 32);
-    r[i] = (uint32_t)c;
-  }
-  return (uint32_t)(c >> 32);
+  for (int i = 0; i < L; i++) r[i] = __builtin_addc(a[i], b[i], c, &c);
+  return c;
 }
 
 // r = a - b over L limbs; returns borrow (1) or 0.
 template <int L>
 ECG_DEV uint32_t sub_limbs(uint32_t* r, const uint32_t* a, const uint32_t* b) {
-  int64_t c = 0;
+  unsigned c = 0;
 #pragma unroll
-  for (int i = 0; i < L; i++) {
-    c = (int64_t)a[i] - b[i] + (c >> 32);
-    r[i] = (uint32_t)c;
-  }
-  return (uint32_t)(c >> 32) & 1;
+  for (int i = 0; i < L; i++) r[i] = __builtin_subc(a[i], b[i], c, &c);
+  return c;
 }
 
 // ---------------------------------------------------------------------------
@@ -126,13 +137,10 @@ template <class P>
 ECG_DEV void reduce_once(Fp<P>& a) {
   constexpr int L = Fp<P>::L;
   uint32_t t[L];
-  int64_t c = 0;
+  unsigned c = 0;
 #pragma unroll
-  for (int i = 0; i < L; i++) {
-    c = (int64_t)a.v[i] - Fp<P>::p32(i) + (c >> 32);
-    t[i] = (uint32_t)c;
-  }
-  bool borrow = (c >> 32) & 1;
+  for (int i = 0; i < L; i++) t[i] = __builtin_subc(a.v[i], Fp<P>::p32(i), c, &c);
+  const bool borrow = c != 0;
 #pragma unroll
   for (int i = 0; i < L; i++) a.v[i] = borrow ? a.v[i] : t[i];
 }
@@ -154,13 +162,10 @@ ECG_DEV Fp<P> fsub(const Fp<P>& a, const Fp<P>& b) {
   Fp<P> r;
   uint32_t borrow = sub_limbs<L>(r.v, a.v, b.v);
   // add p back if borrowed (masked add keeps the code branch-free)
-  uint32_t mask = 0u - borrow;
-  uint64_t c = 0;
+  const uint32_t mask = 0u - borrow;
+  unsigned c = 0;
 #pragma unroll
-  for (int i = 0; i < L; i++) {
-    c = (uint64_t)r.v[i] + (Fp<P>::p32(i) & mask) + (c >> 32);
-    r.v[i] = (uint32_t)c;
-  }
+  for (int i = 0; i < L; i++) r.v[i] = __builtin_addc(r.v[i], Fp<P>::p32(i) & mask, c, &c);
   return r;
 }
 
@@ -279,7 +284,7 @@ ECG_DEV void fmul_column(uint64_t& acc, uint32_t& top, const uint32_t* a, const 
     mac_list<NMP, true>(acc, top, xm, pm);
   }
   if constexpr (K < L) {
-    m[K] = (uint32_t)acc * Fp<P>::inv32();
+    m[K] = mont_digit<P>((uint32_t)acc);
     mac96s(acc, top, m[K], Fp<P>::p32(0));  // low word of acc becomes 0
   } else {
     r[K - L] = (uint32_t)acc;
@@ -328,7 +333,7 @@ ECG_DEV Fp<P> fmul(const Fp<P>& a, const Fp<P>& b) {
     for (int i = 0; i <= k; i++) mac96(acc, top, a.v[i], b.v[k - i]);
 #pragma unroll
     for (int i = 0; i < k; i++) mac96s(acc, top, m[i], Fp<P>::p32(k - i));
-    m[k] = (uint32_t)acc * Fp<P>::inv32();
+    m[k] = mont_digit<P>((uint32_t)acc);
     mac96s(acc, top, m[k], Fp<P>::p32(0));
     acc = (acc >> 32) | ((uint64_t)top << 32);
     top = 0;

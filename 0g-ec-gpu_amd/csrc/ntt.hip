@@ -2,23 +2,27 @@
 //
 // Replaces FIELD_radix_fft (ag-build/cl/fft.cl:4-68) and its host driver
 // SingleFftKernel::radix_fft (ec-gpu-proxy/src/fft.rs:50-135).  Same
-// decomposition (Stockham autosort, natural order in and out, passes of up to
-// 2^8 points), re-designed for gfx950:
+// decomposition (Stockham autosort: natural order in and out, each pass a
+// batch of independent 2^deg-point DFTs between a strided gather and a
+// scatter), re-designed for gfx950:
 //
-//  * A workgroup owns G = TILE >> DEG consecutive Stockham groups (TILE = 1024
-//    elements = 32 KiB of LDS).  Lanes walk the G groups fastest, so every
-//    global read of x[g + i*t] is a G*32-byte contiguous run and the writes
-//    are contiguous runs of min(p, G)*32 bytes (first pass: whole 2^DEG*32 B
-//    groups).  The reference uses one group per block (fft.rs:104-118).
-//  * No per-thread exponentiation: the reference computes twiddle^counts with
-//    FIELD_pow_lookup + FIELD_pow per thread (fft.cl:39-45, about 4x the
-//    butterfly work).  Here inter-pass twiddles w^e (e < n) come from two
-//    precomputed tables, w^e = T_hi[e >> S] * T_lo[e & (2^S-1)] (2 muls per
-//    element, L2-resident), and the in-group roots pq[] sit in LDS.
-//  * Elements live in LDS as two 16-byte planes (conflict-free ds_read_b128
-//    for consecutive indices); DIF butterflies run DEG rounds in LDS and the
-//    final bit-reversal is folded into the output index (fft.cl:64-67).
-//  * Values stay fully reduced (< r) so the output bytes equal serial_fft's.
+//  * v2 (default): radix up to 2^12 per pass, so 2^24 is TWO passes (the
+//    reference uses radix-2^8, three passes, fft.rs:15) -- one fewer twiddled
+//    pass and no odd-pass copy back.  A 2^12-point group lives in 128 KiB of
+//    LDS (two 16-byte planes) worked by a 1024-thread workgroup; smaller
+//    radices put G = 1024/2^deg groups in a workgroup so every global read is
+//    a G*32-byte run.  Each thread runs TWO DIF rounds per LDS round trip on 4
+//    register-resident elements (radix-2^2 step), halving LDS traffic and
+//    barriers.
+//  * No per-thread exponentiation (the reference's FIELD_pow_lookup + FIELD_pow
+//    per thread, fft.cl:39-45, ~4x the butterfly work): inter-pass twiddles
+//    w^e (e < n) = T_hi[e >> 12] * T_lo[e & 4095] from L2-resident tables;
+//    in-group roots from a 2^(maxdeg-1) table.  Tables are built on the device
+//    once per (omega, log n) and cached in the context.
+//  * Values stay fully reduced (< r): output bytes equal serial_fft's.
+//  * v1 (ECG_NTT_VARIANT=1): radix-2^8 passes, one DIF round per LDS round
+//    trip -- kept for A/B measurement.
+#include <cstdlib>
 #include <cstring>
 
 #include "ctx.hpp"
@@ -26,10 +30,7 @@
 
 namespace ecg {
 
-constexpr int NTT_THREADS = 256;
-constexpr int NTT_TILE_LOG = 10;  // 1024 elements per workgroup tile
-constexpr int NTT_MAX_DEG = 8;    // radix-256 passes (MAX_LOG2_RADIX, fft.rs:15)
-constexpr int NTT_LO_BITS = 12;   // twiddle split table size 2^12
+constexpr int NTT_LO_BITS = 12;  // twiddle split table size 2^12
 
 template <class F>
 struct LdsPlanes {
@@ -50,12 +51,61 @@ struct LdsPlanes {
 
 ECG_DEV uint32_t bitrev(uint32_t x, int bits) { return __builtin_bitreverse32(x) >> (32 - bits); }
 
-// One Stockham pass: groups g in [blockIdx.x*G, +G), G = 2^log_g.
+// twiddle w^e for e < n from the split tables
+template <class F>
+ECG_DEV F twiddle(const F* __restrict__ tw_lo, const F* __restrict__ tw_hi, uint64_t e) {
+  return fmul(load(&tw_hi[e >> NTT_LO_BITS]), load(&tw_lo[e & ((1u << NTT_LO_BITS) - 1)]));
+}
+
+// ---------------------------------------------------------------------------
+// shared load / store phases of a Stockham pass
 //   u[i] = x[g + i*t] * w^((n >> (lgp+DEG)) * k * i),  k = g mod 2^lgp, t = n >> DEG
-//   v = DFT_{2^DEG}(u)  (root w^(n >> DEG))
-//   y[(g - k)*2^DEG + k + j*2^lgp] = v[j]
+//   y[(g - k)*2^DEG + k + j*2^lgp] = v[j]   (v = DFT of u, natural order)
+// ---------------------------------------------------------------------------
+template <class F, int DEG>
+ECG_DEV void pass_load(const F* __restrict__ x, const F* __restrict__ tw_lo, const F* __restrict__ tw_hi,
+                       const LdsPlanes<F>& U, uint32_t log_n, uint32_t lgp, uint32_t log_g, uint32_t E) {
+  const uint32_t G = 1u << log_g;
+  const uint64_t t = (1ull << log_n) >> DEG;
+  const uint64_t p = 1ull << lgp;
+  const uint64_t g0 = (uint64_t)blockIdx.x << log_g;
+  const uint32_t s_tw_log = log_n - lgp - DEG;  // n >> (lgp + DEG) = 2^s_tw_log
+  for (uint32_t f = threadIdx.x; f < E; f += blockDim.x) {
+    const uint32_t gi = f & (G - 1), i = f >> log_g;
+    const uint64_t g = g0 + gi;
+    F v = load(&x[g + (uint64_t)i * t]);
+    if (lgp != 0) {
+      const uint64_t e = ((g & (p - 1)) * i) << s_tw_log;  // < n
+      if (e != 0) v = fmul(v, twiddle(tw_lo, tw_hi, e));
+    }
+    U.put((gi << DEG) + i, v);
+  }
+}
+
+template <class F, int DEG>
+ECG_DEV void pass_store(F* __restrict__ y, const LdsPlanes<F>& U, uint32_t lgp, uint32_t log_g, uint32_t E) {
+  constexpr uint32_t R = 1u << DEG;
+  const uint64_t p = 1ull << lgp;
+  const uint64_t g0 = (uint64_t)blockIdx.x << log_g;
+  const uint32_t lpp = lgp < log_g ? lgp : log_g;  // lanes walk min(p, G) fastest -> contiguous runs
+  const uint32_t pp = 1u << lpp;
+  for (uint32_t f = threadIdx.x; f < E; f += blockDim.x) {
+    const uint32_t kk = f & (pp - 1);
+    const uint32_t j = (f >> lpp) & (R - 1);
+    const uint32_t gh = f >> (lpp + DEG);
+    const uint32_t gi = (gh << lpp) + kk;
+    const uint64_t g = g0 + gi;
+    const uint64_t k = g & (p - 1);
+    store(&y[((g - k) << DEG) + k + (uint64_t)j * p], U.get((gi << DEG) + bitrev(j, DEG)));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// v2 pass: DEG <= 12, two DIF rounds per LDS round trip
+// ---------------------------------------------------------------------------
+// threads per workgroup = max(2^DEG, 1024) / 4 (see launch_pass)
 template <class P, int DEG>
-__global__ void __launch_bounds__(NTT_THREADS)
+__global__ void __launch_bounds__(DEG >= 12 ? 1024 : DEG == 11 ? 512 : 256)
     ntt_pass_kernel(const Fp<P>* __restrict__ x, Fp<P>* __restrict__ y, const Fp<P>* __restrict__ pq,
                     uint32_t pq_shift, const Fp<P>* __restrict__ tw_lo, const Fp<P>* __restrict__ tw_hi,
                     uint32_t log_n, uint32_t lgp, uint32_t log_g) {
@@ -63,69 +113,88 @@ __global__ void __launch_bounds__(NTT_THREADS)
   static_assert(F::L == 8, "NTT tiles assume 32-byte scalar-field elements");
   constexpr uint32_t R = 1u << DEG;
   extern __shared__ uint4 smem[];
-  const uint32_t G = 1u << log_g;
-  const uint32_t E = G << DEG;
+  const uint32_t E = R << log_g;
   LdsPlanes<F> U{smem, smem + E};
-  LdsPlanes<F> W{smem + 2 * E, smem + 2 * E + R / 2};
 
-  const uint64_t n = 1ull << log_n;
-  const uint64_t t = n >> DEG;
-  const uint64_t p = 1ull << lgp;
-  const uint64_t g0 = (uint64_t)blockIdx.x << log_g;
-  const uint32_t tid = threadIdx.x;
-
-  // in-group roots w_{2^DEG}^j, j < R/2 (pq is for 2^max_deg: stride pq_shift)
-  for (uint32_t j = tid; j < R / 2; j += NTT_THREADS) W.put(j, load(&pq[(uint64_t)j << pq_shift]));
-
-  // load (+ inter-pass twiddle), lanes walk the G groups fastest
-  const uint32_t s_tw_log = log_n - lgp - DEG;  // n >> (lgp + DEG) = 2^s_tw_log
-  for (uint32_t f = tid; f < E; f += NTT_THREADS) {
-    const uint32_t gi = f & (G - 1), i = f >> log_g;
-    const uint64_t g = g0 + gi;
-    F v = load(&x[g + (uint64_t)i * t]);
-    if (lgp != 0) {
-      const uint64_t k = g & (p - 1);
-      const uint64_t e = (k * i) << s_tw_log;  // < n
-      if (e != 0) {
-        F w = fmul(load(&tw_hi[e >> NTT_LO_BITS]), load(&tw_lo[e & ((1u << NTT_LO_BITS) - 1)]));
-        v = fmul(v, w);
-      }
-    }
-    U.put((gi << DEG) + i, v);
-  }
+  pass_load<F, DEG>(x, tw_lo, tw_hi, U, log_n, lgp, log_g, E);
   __syncthreads();
 
-  // DIF radix-2 rounds (fft.cl:48-62)
+  // radix-2^2 steps: rounds r and r+1 of the DIF network on quartets
+  // {j, j+h, j+2h, j+3h} (h = bit/2, bit = R/2 >> r); root w = w_{2^DEG}.
+  int r = 0;
+  constexpr uint32_t RQ = R >= 4 ? R / 4 : 1;  // quartets per group
+#pragma unroll 1
+  for (; r + 1 < DEG; r += 2) {
+    const uint32_t bit = (R / 2) >> r, h = bit >> 1;
+    for (uint32_t f = threadIdx.x; f < E / 4; f += blockDim.x) {
+      const uint32_t gi = f / RQ, q = f % RQ;
+      const uint32_t qm = q & (h - 1);
+      const uint32_t j = (gi << DEG) + ((q / h) * (2 * bit)) + qm;
+      F e0 = U.get(j), e1 = U.get(j + h), e2 = U.get(j + bit), e3 = U.get(j + bit + h);
+      // round r: (e0, e2) twiddle w^(qm << r), (e1, e3) twiddle w^((qm + h) << r)
+      F s0 = fadd(e0, e2), d0 = fsub(e0, e2);
+      F s1 = fadd(e1, e3), d1 = fsub(e1, e3);
+      if (qm != 0) d0 = fmul(d0, load(&pq[(uint64_t)(qm << r) << pq_shift]));
+      d1 = fmul(d1, load(&pq[(uint64_t)((qm + h) << r) << pq_shift]));
+      // round r+1: pairs (s0, s1) and (d0, d1), both twiddle w^(qm << (r+1))
+      F a0 = fadd(s0, s1), a1 = fsub(s0, s1);
+      F b0 = fadd(d0, d1), b1 = fsub(d0, d1);
+      if (qm != 0) {
+        const F w2 = load(&pq[(uint64_t)(qm << (r + 1)) << pq_shift]);
+        a1 = fmul(a1, w2);
+        b1 = fmul(b1, w2);
+      }
+      U.put(j, a0);
+      U.put(j + h, a1);
+      U.put(j + bit, b0);
+      U.put(j + bit + h, b1);
+    }
+    __syncthreads();
+  }
+  if (r < DEG) {  // odd DEG: last radix-2 round (bit = 1, all twiddles trivial)
+    for (uint32_t f = threadIdx.x; f < E / 2; f += blockDim.x) {
+      const uint32_t i0 = 2 * f;
+      F u0 = U.get(i0), u1 = U.get(i0 + 1);
+      U.put(i0, fadd(u0, u1));
+      U.put(i0 + 1, fsub(u0, u1));
+    }
+    __syncthreads();
+  }
+  pass_store<F, DEG>(y, U, lgp, log_g, E);
+}
+
+// ---------------------------------------------------------------------------
+// v1 pass (A/B): radix-2^8, one radix-2 round per LDS round trip, 256 threads
+// ---------------------------------------------------------------------------
+template <class P, int DEG>
+__global__ void __launch_bounds__(256)
+    ntt_pass_v1_kernel(const Fp<P>* __restrict__ x, Fp<P>* __restrict__ y, const Fp<P>* __restrict__ pq,
+                       uint32_t pq_shift, const Fp<P>* __restrict__ tw_lo, const Fp<P>* __restrict__ tw_hi,
+                       uint32_t log_n, uint32_t lgp, uint32_t log_g) {
+  using F = Fp<P>;
+  constexpr uint32_t R = 1u << DEG;
+  extern __shared__ uint4 smem[];
+  const uint32_t E = R << log_g;
+  LdsPlanes<F> U{smem, smem + E};
+  pass_load<F, DEG>(x, tw_lo, tw_hi, U, log_n, lgp, log_g, E);
+  __syncthreads();
 #pragma unroll 1
   for (int rnd = 0; rnd < DEG; rnd++) {
     const uint32_t bit = (R / 2) >> rnd;
-    for (uint32_t f = tid; f < E / 2; f += NTT_THREADS) {
+    for (uint32_t f = threadIdx.x; f < E / 2; f += blockDim.x) {
       const uint32_t gi = f >> (DEG - 1), b = f & (R / 2 - 1);
       const uint32_t di = b & (bit - 1);
       const uint32_t i0 = (gi << DEG) + (b << 1) - di, i1 = i0 + bit;
       F u0 = U.get(i0), u1 = U.get(i1);
       F s = fadd(u0, u1);
       F d = fsub(u0, u1);
-      if (di != 0) d = fmul(d, W.get(di << rnd));
+      if (di != 0) d = fmul(d, load(&pq[(uint64_t)(di << rnd) << pq_shift]));
       U.put(i0, s);
       U.put(i1, d);
     }
     __syncthreads();
   }
-
-  // store: y[(g - k)*R + k + j*p] = u[bitrev(j)], lanes walk min(p, G) fastest
-  const uint32_t lpp = lgp < log_g ? lgp : log_g;  // log2 min(p, G)
-  const uint32_t pp = 1u << lpp;
-  for (uint32_t f = tid; f < E; f += NTT_THREADS) {
-    const uint32_t kk = f & (pp - 1);
-    const uint32_t j = (f >> lpp) & (R - 1);
-    const uint32_t gh = f >> (lpp + DEG);
-    const uint32_t gi = (gh << lpp) + kk;
-    const uint64_t g = g0 + gi;
-    const uint64_t k = g & (p - 1);
-    F v = U.get((gi << DEG) + bitrev(j, DEG));
-    store(&y[((g - k) << DEG) + k + (uint64_t)j * p], v);
-  }
+  pass_store<F, DEG>(y, U, lgp, log_g, E);
 }
 
 // out[j] = w^(j << shift), j < count  (w given by value, Montgomery)
@@ -133,9 +202,8 @@ template <class P>
 __global__ void ntt_powers_kernel(Fp<P> w, uint32_t shift, uint64_t count, Fp<P>* __restrict__ out) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= count) return;
-  // base = w^(2^shift)
   Fp<P> base = w;
-  for (uint32_t s = 0; s < shift; s++) base = fsqr(base);
+  for (uint32_t s = 0; s < shift; s++) base = fsqr(base);  // base = w^(2^shift)
   Fp<P> r = Fp<P>::one();
   uint64_t e = j;
   while (e) {
@@ -146,99 +214,177 @@ __global__ void ntt_powers_kernel(Fp<P> w, uint32_t shift, uint64_t count, Fp<P>
   store(&out[j], r);
 }
 
-template <class P, int DEG>
-static hipError_t launch_pass(const void* x, void* y, const void* pq, uint32_t pq_shift, const void* tw_lo,
-                              const void* tw_hi, uint32_t log_n, uint32_t lgp, hipStream_t s) {
+// ---------------------------------------------------------------------------
+// launch helpers
+// ---------------------------------------------------------------------------
+struct PassArgs {
+  const void* x;
+  void* y;
+  const void* pq;
+  uint32_t pq_shift;
+  const void* tw_lo;
+  const void* tw_hi;
+  uint32_t log_n, lgp;
+};
+
+template <class P, int DEG, bool V1>
+static hipError_t launch_pass(const PassArgs& a, hipStream_t s) {
   using F = Fp<P>;
-  uint32_t log_g = NTT_TILE_LOG - DEG;
-  const uint32_t log_groups = log_n - DEG;
+  const uint32_t tile_log = V1 ? 10 : (DEG > 10 ? DEG : 10);  // elements per workgroup
+  uint32_t log_g = tile_log - DEG;
+  const uint32_t log_groups = a.log_n - DEG;
   if (log_g > log_groups) log_g = log_groups;
+  const uint32_t E = 1u << (DEG + log_g);
   const uint64_t blocks = 1ull << (log_groups - log_g);
-  const size_t lds = ((size_t)2 << (log_g + DEG)) * sizeof(uint4) + (size_t)(1u << DEG) * sizeof(uint4);
-  hipLaunchKernelGGL((ntt_pass_kernel<P, DEG>), dim3((uint32_t)blocks), dim3(NTT_THREADS), lds, s,
-                     (const F*)x, (F*)y, (const F*)pq, pq_shift, (const F*)tw_lo, (const F*)tw_hi, log_n, lgp,
-                     log_g);
+  const size_t lds = (size_t)2 * E * sizeof(uint4);
+  uint32_t threads;
+  if (V1) {
+    threads = 256;
+  } else {
+    threads = E / 4;
+    if (threads < 64) threads = 64;
+    if (threads > 1024) threads = 1024;
+  }
+  auto kern = V1 ? ntt_pass_v1_kernel<P, DEG> : ntt_pass_kernel<P, DEG>;
+  static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(threads), lds, s, (const F*)a.x, (F*)a.y, (const F*)a.pq,
+                     a.pq_shift, (const F*)a.tw_lo, (const F*)a.tw_hi, a.log_n, a.lgp, log_g);
   return hipGetLastError();
 }
 
-template <class P>
-static hipError_t launch_pass_deg(int deg, const void* x, void* y, const void* pq, uint32_t pq_shift,
-                                  const void* tw_lo, const void* tw_hi, uint32_t log_n, uint32_t lgp,
-                                  hipStream_t s) {
+template <class P, bool V1>
+static hipError_t launch_pass_deg(int deg, const PassArgs& a, hipStream_t s) {
   switch (deg) {
-    case 1: return launch_pass<P, 1>(x, y, pq, pq_shift, tw_lo, tw_hi, log_n, lgp, s);
-    case 2: return launch_pass<P, 2>(x, y, pq, pq_shift, tw_lo, tw_hi, log_n, lgp, s);
-    case 3: return launch_pass<P, 3>(x, y, pq, pq_shift, tw_lo, tw_hi, log_n, lgp, s);
-    case 4: return launch_pass<P, 4>(x, y, pq, pq_shift, tw_lo, tw_hi, log_n, lgp, s);
-    case 5: return launch_pass<P, 5>(x, y, pq, pq_shift, tw_lo, tw_hi, log_n, lgp, s);
-    case 6: return launch_pass<P, 6>(x, y, pq, pq_shift, tw_lo, tw_hi, log_n, lgp, s);
-    case 7: return launch_pass<P, 7>(x, y, pq, pq_shift, tw_lo, tw_hi, log_n, lgp, s);
-    case 8: return launch_pass<P, 8>(x, y, pq, pq_shift, tw_lo, tw_hi, log_n, lgp, s);
+    case 1: return launch_pass<P, 1, V1>(a, s);
+    case 2: return launch_pass<P, 2, V1>(a, s);
+    case 3: return launch_pass<P, 3, V1>(a, s);
+    case 4: return launch_pass<P, 4, V1>(a, s);
+    case 5: return launch_pass<P, 5, V1>(a, s);
+    case 6: return launch_pass<P, 6, V1>(a, s);
+    case 7: return launch_pass<P, 7, V1>(a, s);
+    case 8: return launch_pass<P, 8, V1>(a, s);
+    case 9: return V1 ? hipErrorInvalidValue : launch_pass<P, 9, false>(a, s);
+    case 10: return V1 ? hipErrorInvalidValue : launch_pass<P, 10, false>(a, s);
+    case 11: return V1 ? hipErrorInvalidValue : launch_pass<P, 11, false>(a, s);
+    case 12: return V1 ? hipErrorInvalidValue : launch_pass<P, 12, false>(a, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+static int ntt_variant() {
+  static int v = [] {
+    const char* e = getenv("ECG_NTT_VARIANT");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  return v;
+}
+
+static uint32_t ntt_max_deg() {  // largest radix exponent per pass (v2), tunable for A/B
+  static uint32_t d = [] {
+    const char* e = getenv("ECG_NTT_MAXDEG");
+    int v = e ? atoi(e) : 10;
+    return (uint32_t)(v < 2 ? 2 : v > 12 ? 12 : v);
+  }();
+  return d;
+}
+
+// Pass degrees: v2 splits log n into ceil(log n / maxdeg) balanced passes;
+// v1 uses radix-2^8 passes like the reference (fft.rs:101-102).
+static int plan_passes(uint32_t log_n, int variant, uint32_t* degs) {
+  if (variant == 1) {
+    int np = 0;
+    for (uint32_t lgp = 0; lgp < log_n;) {
+      const uint32_t d = log_n - lgp < 8 ? log_n - lgp : 8;
+      degs[np++] = d;
+      lgp += d;
+    }
+    return np;
+  }
+  const uint32_t md = ntt_max_deg();
+  const int np = (int)((log_n + md - 1) / md);
+  for (int k = 0; k < np; k++) degs[k] = log_n / np + ((uint32_t)k < log_n % np ? 1 : 0);
+  return np;
 }
 
 template <class P>
 static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uint32_t log_n,
                      hipStream_t s, ecg_abort_cb abort_cb, void* user) {
   using F = Fp<P>;
-  if (log_n == 0) {
-    // fft.rs:68-70: pq has length 0 -> the reference panics on pq[0]
-    set_error("radix_fft: log_n must be >= 1");
-    return ECG_ERR_INVALID;
-  }
-  if (log_n > (uint32_t)P::TWO_ADICITY || log_n > 32) {
-    set_error("radix_fft: log_n %u exceeds the field's two-adicity", log_n);
-    return ECG_ERR_INVALID;
-  }
-  const uint64_t n = 1ull << log_n;
-  const uint32_t max_deg = log_n < (uint32_t)NTT_MAX_DEG ? log_n : NTT_MAX_DEG;
-  const uint32_t lo_bits = NTT_LO_BITS;
-  const uint64_t lo_cnt = 1ull << lo_bits;
-  const uint64_t hi_cnt = n > lo_cnt ? (n >> lo_bits) : 1;
-  const uint64_t pq_cnt = 1ull << (max_deg - 1);
+  const int variant = ntt_variant();
+  uint32_t degs[40];
+  const int np = plan_passes(log_n, variant, degs);
+  uint32_t max_deg = 0;
+  for (int k = 0; k < np; k++) max_deg = degs[k] > max_deg ? degs[k] : max_deg;
 
-  void *scratch, *tables;
-  ECG_TRY(ws_get(ctx, "ntt_scratch", n * sizeof(F), &scratch));
+  const uint64_t n = 1ull << log_n;
+  const uint64_t lo_cnt = 1ull << NTT_LO_BITS;
+  const uint64_t hi_cnt = n > lo_cnt ? (n >> NTT_LO_BITS) : 1;
+  const uint64_t pq_cnt = max_deg > 1 ? 1ull << (max_deg - 1) : 1;
+
+  void *scratch = nullptr, *scratch2 = nullptr, *tables;
+  if (np > 1 || variant == 1) ECG_TRY(ws_get(ctx, "ntt_scratch", n * sizeof(F), &scratch));
+  // odd pass counts (> 1) rotate through a second scratch buffer so the last
+  // pass writes d_data directly (no copy back; HBM is plentiful)
+  if (np > 1 && (np & 1)) ECG_TRY(ws_get(ctx, "ntt_scratch2", n * sizeof(F), &scratch2));
   ECG_TRY(ws_get(ctx, "ntt_tables", (pq_cnt + lo_cnt + hi_cnt) * sizeof(F), &tables));
   F* pq = (F*)tables;
   F* tw_lo = pq + pq_cnt;
   F* tw_hi = tw_lo + lo_cnt;
 
-  const bool cached = ctx->tw_fid == field_id && ctx->tw_log_n == log_n &&
+  const bool cached = ctx->tw_fid == field_id && ctx->tw_log_n == log_n && ctx->tw_variant == variant &&
                       memcmp(ctx->tw_omega, omega, sizeof(ctx->tw_omega)) == 0;
   if (!cached) {
     F w;
     memcpy(w.v, omega, sizeof(w.v));
-    // pq[j] = w^(j * (n >> max_deg)) (fft.rs:68-78); tw_lo[j] = w^j; tw_hi[j] = w^(j << lo_bits)
+    // pq[j] = w^(j * (n >> max_deg)) (fft.rs:68-78); tw_lo[j] = w^j; tw_hi[j] = w^(j << 12)
     hipLaunchKernelGGL(ntt_powers_kernel<P>, dim3((uint32_t)((pq_cnt + 255) / 256)), dim3(256), 0, s, w,
                        log_n - max_deg, pq_cnt, pq);
     hipLaunchKernelGGL(ntt_powers_kernel<P>, dim3((uint32_t)((lo_cnt + 255) / 256)), dim3(256), 0, s, w, 0u,
                        lo_cnt, tw_lo);
     hipLaunchKernelGGL(ntt_powers_kernel<P>, dim3((uint32_t)((hi_cnt + 255) / 256)), dim3(256), 0, s, w,
-                       lo_bits, hi_cnt, tw_hi);
+                       (uint32_t)NTT_LO_BITS, hi_cnt, tw_hi);
     ECG_HIP(hipGetLastError());
     ctx->tw_fid = field_id;
     ctx->tw_log_n = log_n;
+    ctx->tw_variant = variant;
     memcpy(ctx->tw_omega, omega, sizeof(ctx->tw_omega));
   }
 
   kt_reset(ctx, "ntt_pass");
-  void* src = d_data;
-  void* dst = scratch;
-  uint32_t lgp = 0;
-  while (lgp < log_n) {
-    if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // fft.rs:94-98
-    const uint32_t deg = (log_n - lgp) < max_deg ? (log_n - lgp) : max_deg;
-    ECG_TRY(kt_begin(ctx, "ntt_pass", s));
-    ECG_HIP(launch_pass_deg<P>((int)deg, src, dst, pq, max_deg - deg, tw_lo, tw_hi, log_n, lgp, s));
-    ECG_TRY(kt_end(ctx, "ntt_pass", s));
-    lgp += deg;
-    void* tmp = src;
-    src = dst;
-    dst = tmp;
+  // Single-pass v2 transforms (log n <= 12) have one workgroup reading every
+  // element before any write: safe in place.  Otherwise ping-pong, arranged so
+  // the last pass lands in d_data whenever the pass count is even.
+  // buffer sequence: d_data -> ... -> d_data
+  void* bufs[41];
+  bufs[0] = d_data;
+  for (int k = 1; k <= np; k++) {
+    if (variant == 1) bufs[k] = (k & 1) ? scratch : d_data;       // ping-pong + copy back (fft.rs:126)
+    else if (np == 1) bufs[k] = d_data;                            // one workgroup: in place
+    else if (k == np) bufs[k] = d_data;                            // last pass lands in place
+    else if (np & 1) bufs[k] = (k & 1) ? scratch : scratch2;       // odd: rotate two scratches
+    else bufs[k] = (k & 1) ? scratch : d_data;                     // even: ping-pong
   }
-  if (src != d_data) ECG_HIP(hipMemcpyAsync(d_data, src, n * sizeof(F), hipMemcpyDeviceToDevice, s));
+  void* src = d_data;
+  void* dst = bufs[1];
+  uint32_t lgp = 0;
+  for (int k = 0; k < np; k++) {
+    if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // fft.rs:94-98
+    src = bufs[k];
+    dst = bufs[k + 1];
+    const PassArgs a{src, dst, pq, max_deg - degs[k], tw_lo, tw_hi, log_n, lgp};
+    ECG_TRY(kt_begin(ctx, "ntt_pass", s));
+    hipError_t e = variant == 1 ? launch_pass_deg<P, true>((int)degs[k], a, s)
+                                : launch_pass_deg<P, false>((int)degs[k], a, s);
+    ECG_HIP(e);
+    ECG_TRY(kt_end(ctx, "ntt_pass", s));
+    lgp += degs[k];
+  }
+  if (bufs[np] != d_data) ECG_HIP(hipMemcpyAsync(d_data, bufs[np], n * sizeof(F), hipMemcpyDeviceToDevice, s));
   return ECG_OK;
 }
 
@@ -264,14 +410,12 @@ int ntt_validate(int field_id, uint32_t log_n) {
 
 int ntt_run(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uint32_t log_n, hipStream_t s,
             ecg_abort_cb abort_cb, void* user) {
+  ECG_TRY(ntt_validate(field_id, log_n));
   switch (field_id) {
     case ECG_FIELD_BLS12_381_FR:
       return ntt_run_t<params::bls12_381_fr>(ctx, field_id, d_data, omega, log_n, s, abort_cb, user);
-    case ECG_FIELD_BN254_FR:
-      return ntt_run_t<params::bn254_fr>(ctx, field_id, d_data, omega, log_n, s, abort_cb, user);
     default:
-      set_error("radix_fft: field_id %d is not an FFT-friendly scalar field", field_id);
-      return ECG_ERR_INVALID;
+      return ntt_run_t<params::bn254_fr>(ctx, field_id, d_data, omega, log_n, s, abort_cb, user);
   }
 }
 
