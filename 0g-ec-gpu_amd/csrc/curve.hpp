@@ -10,6 +10,11 @@
 // are bit-identical to the reference's multiexp_cpu after into_affine()
 // (ec-gpu-proxy/tests/multiexp.rs:99).
 //
+// Every formula takes an arithmetic policy LZ: false = fully reduced field
+// ops (field.hpp strict), true = lazy [0, 2p] representation (field.hpp
+// "Lazy"), which the MSM bucket pipeline uses; values are canonicalised
+// before they leave the pipeline.
+//
 // Identity: ZZ == 0 (XYZZ), Z == 0 (Jacobian, as ec.cl's POINT_ZERO=(0,1,0)),
 // and the all-zero affine pair (ag-types/src/impls.rs:52-54 GpuRepr).
 #pragma once
@@ -28,6 +33,32 @@ struct CurveCfg {
 
 using BLS12_381 = CurveCfg<params::bls12_381_fq, params::bls12_381_fr, params::bls12_381_g1>;
 using BN254 = CurveCfg<params::bn254_fq, params::bn254_fr, params::bn254_g1>;
+
+// Field-op policy
+template <class F, bool LZ>
+struct Ops {
+  using P = typename F::Params;
+  static ECG_DEV F mul(const F& a, const F& b) {
+    if constexpr (LZ) return fmul_lz(a, b); else return fmul(a, b);
+  }
+  static ECG_DEV F sqr(const F& a) { return mul(a, a); }
+  static ECG_DEV F add(const F& a, const F& b) {
+    if constexpr (LZ) return fadd_lz(a, b); else return fadd(a, b);
+  }
+  static ECG_DEV F sub(const F& a, const F& b) {
+    if constexpr (LZ) return fsub_lz(a, b); else return fsub(a, b);
+  }
+  static ECG_DEV F dbl(const F& a) { return add(a, a); }
+  static ECG_DEV F neg(const F& a) {
+    if constexpr (LZ) return fneg_lz(a); else return fneg(a);
+  }
+  static ECG_DEV bool is_zero(const F& a) {
+    if constexpr (LZ) return fis_zero_lz(a); else return fis_zero(a);
+  }
+  static ECG_DEV F canon(const F& a) {
+    if constexpr (LZ) return freduce_full(a); else return a;
+  }
+};
 
 template <class F>
 struct Affine {
@@ -59,9 +90,9 @@ ECG_DEV XYZZ<F> xyzz_zero() {
   return r;
 }
 
-template <class F>
+template <class F, bool LZ = false>
 ECG_DEV bool xyzz_is_zero(const XYZZ<F>& p) {
-  return fis_zero(p.ZZ);
+  return Ops<F, LZ>::is_zero(p.ZZ);
 }
 
 template <class F>
@@ -75,113 +106,127 @@ ECG_DEV XYZZ<F> xyzz_from_affine(const Affine<F>& a) {
 }
 
 // mdbl-2008-s-1 (affine input, a = 0): 2 * (x, y)
-template <class F>
+template <class F, bool LZ = false>
 ECG_DEV XYZZ<F> xyzz_dbl_affine(const Affine<F>& a) {
-  F U = fdbl(a.y);
-  F V = fsqr(U);
-  F W = fmul(U, V);
-  F S = fmul(a.x, V);
-  F X2 = fsqr(a.x);
-  F M = fadd(fdbl(X2), X2);
+  using O = Ops<F, LZ>;
+  F U = O::dbl(a.y);
+  F V = O::sqr(U);
+  F W = O::mul(U, V);
+  F S = O::mul(a.x, V);
+  F X2 = O::sqr(a.x);
+  F M = O::add(O::dbl(X2), X2);
   XYZZ<F> r;
-  r.X = fsub(fsub(fsqr(M), S), S);
-  r.Y = fsub(fmul(M, fsub(S, r.X)), fmul(W, a.y));
+  r.X = O::sub(O::sub(O::sqr(M), S), S);
+  r.Y = O::sub(O::mul(M, O::sub(S, r.X)), O::mul(W, a.y));
   r.ZZ = V;
   r.ZZZ = W;
   return r;
 }
 
 // dbl-2008-s-1 (a = 0): 2 * P
-template <class F>
+template <class F, bool LZ = false>
 ECG_DEV XYZZ<F> xyzz_dbl(const XYZZ<F>& p) {
-  if (xyzz_is_zero(p)) return p;
-  F U = fdbl(p.Y);
-  F V = fsqr(U);
-  F W = fmul(U, V);
-  F S = fmul(p.X, V);
-  F X2 = fsqr(p.X);
-  F M = fadd(fdbl(X2), X2);
+  using O = Ops<F, LZ>;
+  if (xyzz_is_zero<F, LZ>(p)) return p;
+  F U = O::dbl(p.Y);
+  F V = O::sqr(U);
+  F W = O::mul(U, V);
+  F S = O::mul(p.X, V);
+  F X2 = O::sqr(p.X);
+  F M = O::add(O::dbl(X2), X2);
   XYZZ<F> r;
-  r.X = fsub(fsub(fsqr(M), S), S);
-  r.Y = fsub(fmul(M, fsub(S, r.X)), fmul(W, p.Y));
-  r.ZZ = fmul(V, p.ZZ);
-  r.ZZZ = fmul(W, p.ZZZ);
+  r.X = O::sub(O::sub(O::sqr(M), S), S);
+  r.Y = O::sub(O::mul(M, O::sub(S, r.X)), O::mul(W, p.Y));
+  r.ZZ = O::mul(V, p.ZZ);
+  r.ZZZ = O::mul(W, p.ZZZ);
   return r;
 }
 
-// madd-2008-s: P + (x2, y2) with y2 optionally negated (signed bucket digit).
-// Handles P = O, P = Q (doubling) and P = -Q (identity).  `a` must not be the
-// identity (callers skip identity bases).
-template <class F>
+// madd-2008-s: P + (x2, y2).  Handles P = O, P = Q (doubling) and P = -Q
+// (identity).  `a` must not be the identity (callers skip identity bases).
+template <class F, bool LZ = false>
 ECG_DEV XYZZ<F> xyzz_add_affine(const XYZZ<F>& p, const Affine<F>& a) {
-  if (xyzz_is_zero(p)) return xyzz_from_affine(a);
-  F U2 = fmul(a.x, p.ZZ);
-  F S2 = fmul(a.y, p.ZZZ);
-  F P = fsub(U2, p.X);
-  F R = fsub(S2, p.Y);
-  if (fis_zero(P)) {
-    if (fis_zero(R)) return xyzz_dbl_affine(a);
+  using O = Ops<F, LZ>;
+  if (xyzz_is_zero<F, LZ>(p)) return xyzz_from_affine(a);
+  F U2 = O::mul(a.x, p.ZZ);
+  F S2 = O::mul(a.y, p.ZZZ);
+  F P = O::sub(U2, p.X);
+  F R = O::sub(S2, p.Y);
+  if (O::is_zero(P)) {
+    if (O::is_zero(R)) return xyzz_dbl_affine<F, LZ>(a);
     return xyzz_zero<F>();
   }
-  F PP = fsqr(P);
-  F PPP = fmul(P, PP);
-  F Q = fmul(p.X, PP);
+  F PP = O::sqr(P);
+  F PPP = O::mul(P, PP);
+  F Q = O::mul(p.X, PP);
   XYZZ<F> r;
-  r.X = fsub(fsub(fsub(fsqr(R), PPP), Q), Q);
-  r.Y = fsub(fmul(R, fsub(Q, r.X)), fmul(p.Y, PPP));
-  r.ZZ = fmul(p.ZZ, PP);
-  r.ZZZ = fmul(p.ZZZ, PPP);
+  r.X = O::sub(O::sub(O::sub(O::sqr(R), PPP), Q), Q);
+  r.Y = O::sub(O::mul(R, O::sub(Q, r.X)), O::mul(p.Y, PPP));
+  r.ZZ = O::mul(p.ZZ, PP);
+  r.ZZZ = O::mul(p.ZZZ, PPP);
   return r;
 }
 
 // add-2008-s: P + Q, both XYZZ.
-template <class F>
+template <class F, bool LZ = false>
 ECG_DEV XYZZ<F> xyzz_add(const XYZZ<F>& p, const XYZZ<F>& q) {
-  if (xyzz_is_zero(p)) return q;
-  if (xyzz_is_zero(q)) return p;
-  F U1 = fmul(p.X, q.ZZ);
-  F U2 = fmul(q.X, p.ZZ);
-  F S1 = fmul(p.Y, q.ZZZ);
-  F S2 = fmul(q.Y, p.ZZZ);
-  F P = fsub(U2, U1);
-  F R = fsub(S2, S1);
-  if (fis_zero(P)) {
-    if (fis_zero(R)) return xyzz_dbl(p);
+  using O = Ops<F, LZ>;
+  if (xyzz_is_zero<F, LZ>(p)) return q;
+  if (xyzz_is_zero<F, LZ>(q)) return p;
+  F U1 = O::mul(p.X, q.ZZ);
+  F U2 = O::mul(q.X, p.ZZ);
+  F S1 = O::mul(p.Y, q.ZZZ);
+  F S2 = O::mul(q.Y, p.ZZZ);
+  F P = O::sub(U2, U1);
+  F R = O::sub(S2, S1);
+  if (O::is_zero(P)) {
+    if (O::is_zero(R)) return xyzz_dbl<F, LZ>(p);
     return xyzz_zero<F>();
   }
-  F PP = fsqr(P);
-  F PPP = fmul(P, PP);
-  F Q = fmul(U1, PP);
+  F PP = O::sqr(P);
+  F PPP = O::mul(P, PP);
+  F Q = O::mul(U1, PP);
   XYZZ<F> r;
-  r.X = fsub(fsub(fsub(fsqr(R), PPP), Q), Q);
-  r.Y = fsub(fmul(R, fsub(Q, r.X)), fmul(S1, PPP));
-  r.ZZ = fmul(fmul(p.ZZ, q.ZZ), PP);
-  r.ZZZ = fmul(fmul(p.ZZZ, q.ZZZ), PPP);
+  r.X = O::sub(O::sub(O::sub(O::sqr(R), PPP), Q), Q);
+  r.Y = O::sub(O::mul(R, O::sub(Q, r.X)), O::mul(S1, PPP));
+  r.ZZ = O::mul(O::mul(p.ZZ, q.ZZ), PP);
+  r.ZZZ = O::mul(O::mul(p.ZZZ, q.ZZZ), PPP);
   return r;
 }
 
-template <class F>
+template <class F, bool LZ = false>
 ECG_DEV XYZZ<F> xyzz_neg(const XYZZ<F>& p) {
   XYZZ<F> r = p;
-  r.Y = fneg(p.Y);
+  r.Y = Ops<F, LZ>::neg(p.Y);
   return r;
 }
 
 // k * P for a small unsigned scalar (double-and-add from the MSB).
-template <class F>
+template <class F, bool LZ = false>
 ECG_DEV XYZZ<F> xyzz_mul_small(const XYZZ<F>& p, uint32_t k) {
   XYZZ<F> acc = xyzz_zero<F>();
-  if (k == 0 || xyzz_is_zero(p)) return acc;
+  if (k == 0 || xyzz_is_zero<F, LZ>(p)) return acc;
   int top = 31 - __builtin_clz(k);
   acc = p;
   for (int b = top - 1; b >= 0; b--) {
-    acc = xyzz_dbl(acc);
-    if ((k >> b) & 1) acc = xyzz_add(acc, p);
+    acc = xyzz_dbl<F, LZ>(acc);
+    if ((k >> b) & 1) acc = xyzz_add<F, LZ>(acc, p);
   }
   return acc;
 }
 
-// XYZZ -> affine (identity -> all-zero pair).
+// Canonicalise every coordinate (lazy [0, 2p] -> [0, p)).
+template <class F>
+ECG_DEV XYZZ<F> xyzz_canon(const XYZZ<F>& p) {
+  XYZZ<F> r;
+  r.X = freduce_full(p.X);
+  r.Y = freduce_full(p.Y);
+  r.ZZ = freduce_full(p.ZZ);
+  r.ZZZ = freduce_full(p.ZZZ);
+  return r;
+}
+
+// XYZZ -> affine (identity -> all-zero pair).  Strict inputs.
 template <class F>
 ECG_DEV Affine<F> xyzz_to_affine(const XYZZ<F>& p) {
   Affine<F> r;

@@ -34,6 +34,7 @@ namespace params {
 
 template <class P>
 struct Fp {
+  using Params = P;
   static constexpr int N = P::N;       // 64-bit limbs
   static constexpr int L = 2 * P::N;   // 32-bit limbs
   uint32_t v[L];
@@ -320,7 +321,8 @@ ECG_DEV Fp<P> fmul_x4(const Fp<P>& a, const Fp<P>& b) {
 
 // Montgomery product a*b*R^-1 mod p, product-scanning (FIPS) form, one
 // product per asm statement (the default: fastest measured form).
-template <class P>
+// REDUCE = false skips the final conditional subtraction (lazy form, below).
+template <class P, bool REDUCE = true>
 ECG_DEV Fp<P> fmul(const Fp<P>& a, const Fp<P>& b) {
   constexpr int L = Fp<P>::L;
   uint32_t m[L];
@@ -349,12 +351,107 @@ ECG_DEV Fp<P> fmul(const Fp<P>& a, const Fp<P>& b) {
     top = 0;
   }
   r.v[L - 1] = (uint32_t)acc;
-  reduce_once(r);
+  if constexpr (REDUCE) reduce_once(r);
   return r;
 }
 
 template <class P>
 ECG_DEV Fp<P> fsqr(const Fp<P>& a) { return fmul(a, a); }
+
+// ---------------------------------------------------------------------------
+// Lazy ("redundant") arithmetic for moduli with 4p < 2^(32L): values live in
+// [0, 2p].  Closed under Montgomery multiplication with NO final subtraction
+// (a, b <= 2p  =>  (ab + mp)/R < 4p^2/R + p < 2p), and add/sub/neg each need
+// one correction by 2p.  Used by the MSM bucket arithmetic over both base
+// fields; every value that leaves the MSM pipeline is canonicalised first
+// (freduce_full), so outputs stay bit-identical to the reference's.
+// ---------------------------------------------------------------------------
+template <class P>
+struct Lazy {
+  static constexpr bool ok() { return (P::P[P::N - 1] >> 62) == 0; }  // p < 2^(64N-2)  <=>  4p < R
+};
+
+// 2p as 32-bit limbs (carry of the 64-bit shift handled explicitly)
+template <class P>
+ECG_DEV constexpr uint32_t p2_limb(int i) {
+  const int w = i >> 1;
+  const uint64_t lo = P::P[w] << 1 | (w > 0 ? P::P[w - 1] >> 63 : 0);
+  return (i & 1) ? (uint32_t)(lo >> 32) : (uint32_t)lo;
+}
+
+template <class P>
+ECG_DEV Fp<P> fmul_lz(const Fp<P>& a, const Fp<P>& b) {
+  static_assert(Lazy<P>::ok(), "lazy reduction needs 4p < R");
+  return fmul<P, false>(a, b);
+}
+
+template <class P>
+ECG_DEV Fp<P> fsqr_lz(const Fp<P>& a) { return fmul_lz(a, a); }
+
+// a + b with a, b in [0, 2p] -> [0, 2p]
+template <class P>
+ECG_DEV Fp<P> fadd_lz(const Fp<P>& a, const Fp<P>& b) {
+  constexpr int L = Fp<P>::L;
+  Fp<P> r;
+  uint32_t t[L];
+  add_limbs<L>(r.v, a.v, b.v);  // < 4p < R: no carry-out
+  unsigned c = 0;
+#pragma unroll
+  for (int i = 0; i < L; i++) t[i] = __builtin_subc(r.v[i], p2_limb<P>(i), c, &c);
+  const bool borrow = c != 0;
+#pragma unroll
+  for (int i = 0; i < L; i++) r.v[i] = borrow ? r.v[i] : t[i];
+  return r;
+}
+
+template <class P>
+ECG_DEV Fp<P> fdbl_lz(const Fp<P>& a) { return fadd_lz(a, a); }
+
+// a - b with a, b in [0, 2p] -> [0, 2p]
+template <class P>
+ECG_DEV Fp<P> fsub_lz(const Fp<P>& a, const Fp<P>& b) {
+  constexpr int L = Fp<P>::L;
+  Fp<P> r;
+  const uint32_t borrow = sub_limbs<L>(r.v, a.v, b.v);
+  const uint32_t mask = 0u - borrow;
+  unsigned c = 0;
+#pragma unroll
+  for (int i = 0; i < L; i++) r.v[i] = __builtin_addc(r.v[i], p2_limb<P>(i) & mask, c, &c);
+  return r;
+}
+
+// 2p - a, a in [0, 2p] -> [0, 2p]: one subtraction, no correction
+template <class P>
+ECG_DEV Fp<P> fneg_lz(const Fp<P>& a) {
+  constexpr int L = Fp<P>::L;
+  Fp<P> r;
+  unsigned c = 0;
+#pragma unroll
+  for (int i = 0; i < L; i++) r.v[i] = __builtin_subc(p2_limb<P>(i), a.v[i], c, &c);
+  return r;
+}
+
+// [0, 2p] -> canonical [0, p)
+template <class P>
+ECG_DEV Fp<P> freduce_full(Fp<P> a) {
+  reduce_once(a);  // [0, 2p] -> [0, p]
+  reduce_once(a);  // p -> 0
+  return a;
+}
+
+// a == 0 (mod p) for a in [0, 2p]
+template <class P>
+ECG_DEV bool fis_zero_lz(const Fp<P>& a) {
+  constexpr int L = Fp<P>::L;
+  uint32_t z = 0, e1 = 0, e2 = 0;
+#pragma unroll
+  for (int i = 0; i < L; i++) {
+    z |= a.v[i];
+    e1 |= a.v[i] ^ Fp<P>::p32(i);
+    e2 |= a.v[i] ^ p2_limb<P>(i);
+  }
+  return z == 0 || e1 == 0 || e2 == 0;
+}
 
 // Portable CIOS reference variant (row-wise u64 chains) -- kept for A/B
 // measurement against the asm product-scanning form (tools/field_bench).

@@ -55,6 +55,13 @@ static inline void sub_p(uint64_t* a) {
   }
 }
 
+// device lazy range [0, 2p] -> canonical [0, p)
+template <class P>
+static inline HFp<P> hcanon(HFp<P> a) {
+  while (geq_p<P>(a.v)) sub_p<P>(a.v);
+  return a;
+}
+
 template <class P>
 static inline HFp<P> hadd(const HFp<P>& a, const HFp<P>& b) {
   HFp<P> r;

@@ -46,10 +46,22 @@
 namespace ecg {
 
 constexpr int MSM_THREADS = 256;
-constexpr uint32_t MSM_SEG = 32;         // buckets per reduction segment
-constexpr uint32_t MSM_ACC_SEG = 64;     // sorted entries per accumulation thread
 constexpr uint32_t MSM_FOLD = 32;        // fan-in of the partial-sum tree
 constexpr size_t MSM_MAX_CHUNK = 1ull << 27;  // terms per device pass
+
+// Tunables (env overrides for A/B measurement in one build).
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* e = getenv(name);
+  return e ? (uint32_t)strtoul(e, nullptr, 10) : dflt;
+}
+static uint32_t msm_red_seg() {  // buckets per reduction segment
+  static uint32_t v = env_u32("ECG_MSM_RED_SEG", 64);
+  return v;
+}
+static uint32_t msm_acc_seg() {  // sorted entries per accumulation thread
+  static uint32_t v = env_u32("ECG_MSM_ACC_SEG", 128);
+  return v;
+}
 
 struct MsmPlan {
   uint32_t c;     // window bits
@@ -57,6 +69,7 @@ struct MsmPlan {
   uint32_t B;     // buckets per window = 2^(c-1)
   uint32_t T;     // reduction segments per window
   uint32_t LS;    // buckets per segment
+  uint32_t seg;   // sorted entries per accumulation thread
 };
 
 // Window size minimising  n*W + W*B*2.8  (bucket accumulation vs reduction
@@ -77,8 +90,9 @@ static MsmPlan make_plan(size_t n, uint32_t nbits) {
     }
   }
   pl.B = 1u << (pl.c - 1);
-  pl.LS = pl.B < MSM_SEG ? pl.B : MSM_SEG;
+  pl.LS = pl.B < msm_red_seg() ? pl.B : msm_red_seg();
   pl.T = pl.B / pl.LS;
+  pl.seg = msm_acc_seg();
   return pl;
 }
 
@@ -160,9 +174,10 @@ __global__ void __launch_bounds__(MSM_THREADS)
 // slot 2t (b is the segment's first key) or 2t+1 (b is its last key).
 template <class C>
 ECG_DEV void acc_flush(uint32_t b, uint32_t first_key, const XYZZ<typename C::Fq>& acc, const uint32_t* start,
-                       const uint32_t* end, size_t t, XYZZ<typename C::Fq>* buckets, XYZZ<typename C::Fq>* recs) {
+                       const uint32_t* end, size_t t, uint32_t seg, XYZZ<typename C::Fq>* buckets,
+                       XYZZ<typename C::Fq>* recs) {
   const uint32_t s0 = start[b], s1 = end[b];
-  if (s0 / MSM_ACC_SEG == (s1 - 1) / MSM_ACC_SEG) {
+  if (s0 / seg == (s1 - 1) / seg) {
     store_xyzz(&buckets[b], acc);
   } else {
     store_xyzz(&recs[2 * t + (b == first_key ? 0 : 1)], acc);
@@ -172,14 +187,14 @@ ECG_DEV void acc_flush(uint32_t b, uint32_t first_key, const XYZZ<typename C::Fq
 template <class C>
 __global__ void __launch_bounds__(MSM_THREADS)
     msm_accumulate_kernel(const typename C::Fq* __restrict__ bases, const uint32_t* __restrict__ keys,
-                          const uint32_t* __restrict__ vals, size_t total, uint32_t sentinel,
+                          const uint32_t* __restrict__ vals, size_t total, uint32_t sentinel, uint32_t seg,
                           const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
                           XYZZ<typename C::Fq>* __restrict__ buckets, XYZZ<typename C::Fq>* __restrict__ recs) {
   using F = typename C::Fq;
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t e0 = t * MSM_ACC_SEG;
+  const size_t e0 = t * seg;
   if (e0 >= total) return;
-  const size_t e1 = e0 + MSM_ACC_SEG < total ? e0 + MSM_ACC_SEG : total;
+  const size_t e1 = e0 + seg < total ? e0 + seg : total;
   const uint32_t first_key = keys[e0];
   if (first_key >= sentinel) return;
   uint32_t b = first_key;
@@ -194,12 +209,12 @@ __global__ void __launch_bounds__(MSM_THREADS)
     Affine<F> Pn;
     if (kn < sentinel) Pn = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
     if (!aff_is_identity(P)) {  // GpuRepr identity (impls.rs:52-54) contributes nothing
-      F ny = fneg(P.y);
+      F ny = fneg_lz(P.y);  // 2p - y: one subtraction (lazy range)
       if (v >> 31) P.y = ny;
-      acc = xyzz_add_affine(acc, P);
+      acc = xyzz_add_affine<F, true>(acc, P);
     }
     if (kn != b) {
-      acc_flush<C>(b, first_key, acc, start, end, t, buckets, recs);
+      acc_flush<C>(b, first_key, acc, start, end, t, seg, buckets, recs);
       if (kn >= sentinel) return;
       acc = xyzz_zero<F>();
       b = kn;
@@ -207,7 +222,7 @@ __global__ void __launch_bounds__(MSM_THREADS)
     P = Pn;
     v = vn;
   }
-  acc_flush<C>(b, first_key, acc, start, end, t, buckets, recs);
+  acc_flush<C>(b, first_key, acc, start, end, t, seg, buckets, recs);
 }
 
 // ---------------------------------------------------------------------------
@@ -216,8 +231,8 @@ __global__ void __launch_bounds__(MSM_THREADS)
 template <class C>
 __global__ void __launch_bounds__(MSM_THREADS)
     msm_fixup_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ start,
-                     const uint32_t* __restrict__ end, uint32_t nbuckets, const XYZZ<typename C::Fq>* __restrict__ recs,
-                     XYZZ<typename C::Fq>* __restrict__ buckets) {
+                     const uint32_t* __restrict__ end, uint32_t nbuckets, uint32_t seg,
+                     const XYZZ<typename C::Fq>* __restrict__ recs, XYZZ<typename C::Fq>* __restrict__ buckets) {
   using F = typename C::Fq;
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nbuckets) return;
@@ -226,12 +241,12 @@ __global__ void __launch_bounds__(MSM_THREADS)
     store_xyzz(&buckets[b], xyzz_zero<F>());
     return;
   }
-  const uint32_t t0 = s0 / MSM_ACC_SEG, t1 = (s1 - 1) / MSM_ACC_SEG;
+  const uint32_t t0 = s0 / seg, t1 = (s1 - 1) / seg;
   if (t0 == t1) return;  // written by msm_accumulate
   XYZZ<F> acc = xyzz_zero<F>();
   for (uint32_t t = t0; t <= t1; t++) {
-    const uint32_t slot = keys[(size_t)t * MSM_ACC_SEG] == b ? 0 : 1;
-    acc = xyzz_add(acc, load_xyzz(&recs[2 * (size_t)t + slot]));
+    const uint32_t slot = keys[(size_t)t * seg] == b ? 0 : 1;
+    acc = xyzz_add<F, true>(acc, load_xyzz(&recs[2 * (size_t)t + slot]));
   }
   store_xyzz(&buckets[b], acc);
 }
@@ -250,11 +265,11 @@ __global__ void __launch_bounds__(MSM_THREADS)
   const XYZZ<F>* bk = buckets + (size_t)w * pl.B + (size_t)sgm * pl.LS;
   XYZZ<F> run = xyzz_zero<F>(), acc = xyzz_zero<F>();
   for (int j = (int)pl.LS - 1; j >= 0; j--) {
-    run = xyzz_add(run, load_xyzz(&bk[j]));
-    acc = xyzz_add(acc, run);
+    run = xyzz_add<F, true>(run, load_xyzz(&bk[j]));
+    acc = xyzz_add<F, true>(acc, run);
   }
   // acc = sum_j (j+1) S_j ; add (sgm*LS) * run for the segment offset
-  if (sgm != 0) acc = xyzz_add(acc, xyzz_mul_small(run, sgm * pl.LS));
+  if (sgm != 0) acc = xyzz_add<F, true>(acc, xyzz_mul_small<F, true>(run, sgm * pl.LS));
   store_xyzz(&partial[id], acc);
 }
 
@@ -271,7 +286,7 @@ __global__ void __launch_bounds__(MSM_THREADS)
   const uint32_t w = id / out_cnt, o = id % out_cnt;
   const uint32_t j0 = o * MSM_FOLD, j1 = min(j0 + MSM_FOLD, cnt);
   XYZZ<F> acc = xyzz_zero<F>();
-  for (uint32_t j = j0; j < j1; j++) acc = xyzz_add(acc, load_xyzz(&in[(size_t)w * cnt + j]));
+  for (uint32_t j = j0; j < j1; j++) acc = xyzz_add<F, true>(acc, load_xyzz(&in[(size_t)w * cnt + j]));
   store_xyzz(&out[id], acc);
 }
 
@@ -375,7 +390,7 @@ static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, s
     const uint32_t sentinel = nb;
     int key_bits = 1;
     while ((1ull << key_bits) <= sentinel) key_bits++;
-    const size_t nseg = (total + MSM_ACC_SEG - 1) / MSM_ACC_SEG;
+    const size_t nseg = (total + pl.seg - 1) / pl.seg;
 
     void *k0, *k1, *v0, *v1, *st, *en, *bk, *rc, *pa, *pb, *tmp;
     ECG_TRY(ws_get(ctx, "msm_k0", total * 4, &k0));
@@ -411,13 +426,14 @@ static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, s
 
     ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
     hipLaunchKernelGGL(msm_accumulate_kernel<C>, dim3(blocks_for(nseg, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                       bases, (const uint32_t*)k1, (const uint32_t*)v1, total, sentinel, (const uint32_t*)st,
+                       bases, (const uint32_t*)k1, (const uint32_t*)v1, total, sentinel, pl.seg, (const uint32_t*)st,
                        (const uint32_t*)en, (X*)bk, (X*)rc);
     ECG_HIP(hipGetLastError());
     ECG_TRY(kt_end(ctx, "msm_accumulate", s));
 
     hipLaunchKernelGGL(msm_fixup_kernel<C>, dim3(blocks_for(nb, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                       (const uint32_t*)k1, (const uint32_t*)st, (const uint32_t*)en, nb, (const X*)rc, (X*)bk);
+                       (const uint32_t*)k1, (const uint32_t*)st, (const uint32_t*)en, nb, pl.seg, (const X*)rc,
+                       (X*)bk);
     ECG_HIP(hipGetLastError());
 
     hipLaunchKernelGGL(msm_reduce_kernel<C>, dim3(blocks_for((size_t)pl.W * pl.T, MSM_THREADS)),
@@ -445,10 +461,15 @@ static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, s
     for (int w = (int)pl.W - 1; w >= 0; w--) {
       for (uint32_t k = 0; k < pl.c; k++) acc = host::hdbl(acc);
       HX ww;
+      // device values are in the lazy range [0, 2p]: canonicalise
       memcpy(ww.X.v, win[w].X.v, sizeof(ww.X.v));
       memcpy(ww.Y.v, win[w].Y.v, sizeof(ww.Y.v));
       memcpy(ww.ZZ.v, win[w].ZZ.v, sizeof(ww.ZZ.v));
       memcpy(ww.ZZZ.v, win[w].ZZZ.v, sizeof(ww.ZZZ.v));
+      ww.X = host::hcanon(ww.X);
+      ww.Y = host::hcanon(ww.Y);
+      ww.ZZ = host::hcanon(ww.ZZ);
+      ww.ZZZ = host::hcanon(ww.ZZZ);
       acc = host::hadd_pts(acc, ww);
     }
     total_acc = host::hadd_pts(total_acc, acc);
