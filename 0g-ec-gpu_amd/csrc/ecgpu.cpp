@@ -347,6 +347,28 @@ int ecg_msm_dev(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_s
   return kt_collect(ctx);
 }
 
+int ecg_multiple_multiexp(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const uint64_t* scalars,
+                          int scalars_on_device, size_t line_len, size_t num_chunks, uint32_t window_bits,
+                          uint64_t* out_jac) {
+  ECG_TRY(ctx_enter(ctx));
+  if (!out_jac || (n_bases && (!d_bases || !scalars))) {
+    set_error("ecg_multiple_multiexp: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  hipStream_t s = ctx->stream;
+  const void* d_sc = scalars;
+  if (!scalars_on_device && n_bases) {  // multiexp.rs:64 in_ref_slice(&exponents)
+    void* d;
+    ECG_TRY(ws_get(ctx, "mmsm_scalars", line_len * 32, &d));
+    ECG_HIP(hipMemcpyAsync(d, scalars, line_len * 32, hipMemcpyHostToDevice, s));
+    d_sc = d;
+  }
+  int rc = msm_batch_run(ctx, curve_id, d_bases, n_bases, d_sc, line_len, num_chunks, window_bits, out_jac, s);
+  (void)hipStreamSynchronize(s);
+  if (rc != ECG_OK) return rc;
+  return kt_collect(ctx);
+}
+
 int ecg_point_sum_dev(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, uint64_t* out_jac,
                       void* stream) {
   ECG_TRY(ctx_enter(ctx));

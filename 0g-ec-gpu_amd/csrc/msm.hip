@@ -67,23 +67,38 @@ struct MsmPlan {
   uint32_t c;     // window bits
   uint32_t W;     // windows
   uint32_t B;     // buckets per window = 2^(c-1)
-  uint32_t T;     // reduction segments per window
+  uint32_t S;     // reduction segments per window
   uint32_t LS;    // buckets per segment
   uint32_t seg;   // sorted entries per accumulation thread
+  uint32_t G;     // bucket groups = tasks * W  (one group per (task, window))
 };
 
-// Window size minimising  n*W + W*B*2.8  (bucket accumulation vs reduction
-// adds, reduction adds ~1.4x a mixed add).  nbits = scalar MODULUS_BIT_SIZE.
-static MsmPlan make_plan(size_t n, uint32_t nbits) {
+// Task geometry.  A single MSM is one task (n_lines = n_chunks = 1).  The
+// batched form is ag-cuda-ec's multiple_multiexp (ag-cuda-ec/src/multiexp.rs:
+// 21-81, kernel ag-build/cl/multiexp.cl:215-262): n_lines lines of line_len
+// bases share one row of line_len scalars; each line is cut into n_chunks
+// chunks of clen = line_len / n_chunks terms (a remainder is ignored, as in
+// multiexp.cl:230), and task (line, chunk) computes
+//   sum_{i < clen} s[chunk*clen + i] * P[line*line_len + chunk*clen + i].
+struct MsmGeom {
+  uint32_t n_lines;
+  uint32_t n_chunks;
+  size_t line_len;
+  size_t clen;
+  uint32_t tasks() const { return n_lines * n_chunks; }
+};
+
+// Window size minimising  n*W + W*B*4 + W*c*12  per task (bucket accumulation
+// vs reduction vs window-fold adds; a reduction step is ~2 full adds, ~1.4x a
+// mixed add).  nbits = scalar MODULUS_BIT_SIZE.  forced_c != 0 pins c.
+static MsmPlan make_plan(size_t n, uint32_t nbits, uint32_t forced_c = 0) {
   double best = 1e300;
   MsmPlan pl{};
-  for (uint32_t c = 2; c <= 22; c++) {
+  for (uint32_t c = 1; c <= 22; c++) {
     uint32_t W = (nbits + 1 + c - 1) / c;
     double B = (double)(1u << (c - 1));
-    // ~3.5 mixed-add equivalents per bucket in the reduction (2 full adds +
-    // the amortised segment scalar multiple), 1 per term per window.
     double cost = (double)n * W + W * B * 4.0 + W * c * 12.0;
-    if (cost < best) {
+    if (forced_c ? c == forced_c : (c >= 2 && cost < best)) {
       best = cost;
       pl.c = c;
       pl.W = W;
@@ -91,21 +106,25 @@ static MsmPlan make_plan(size_t n, uint32_t nbits) {
   }
   pl.B = 1u << (pl.c - 1);
   pl.LS = pl.B < msm_red_seg() ? pl.B : msm_red_seg();
-  pl.T = pl.B / pl.LS;
+  pl.S = pl.B / pl.LS;
   pl.seg = msm_acc_seg();
+  pl.G = pl.W;
   return pl;
 }
 
 // ---------------------------------------------------------------------------
 // 1. signed-digit decomposition
 // ---------------------------------------------------------------------------
+// One thread per scalar j of the row; the digits are emitted once per line
+// (entry (w, line, j) -> key = group(line, chunk(j), w) * B + |d| - 1).
 template <class C>
 __global__ void __launch_bounds__(MSM_THREADS)
-    msm_digits_kernel(const uint4* __restrict__ scalars, size_t n, MsmPlan pl, uint32_t* __restrict__ keys,
+    msm_digits_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, uint32_t* __restrict__ keys,
                       uint32_t* __restrict__ vals) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint4 lo = scalars[2 * i], hi = scalars[2 * i + 1];
+  const size_t m = (size_t)g.n_chunks * g.clen;
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  uint4 lo = scalars[2 * j], hi = scalars[2 * j + 1];
   uint32_t s[9] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, 0};
   // reduce mod r (any 256-bit input; at most 2^256/r subtractions)
   using FrP = typename C::FrParams;
@@ -121,9 +140,10 @@ __global__ void __launch_bounds__(MSM_THREADS)
 #pragma unroll
     for (int k = 0; k < 8; k++) s[k] = t[k];
   }
+  const uint32_t chunk = g.n_chunks == 1 ? 0u : (uint32_t)(j / g.clen);
   const uint32_t mask = (1u << pl.c) - 1;
   const uint32_t half = 1u << (pl.c - 1);
-  const uint32_t sentinel = pl.W * pl.B;
+  const uint32_t sentinel = pl.G * pl.B;
   uint32_t carry = 0;
   for (uint32_t w = 0; w < pl.W; w++) {
     const uint32_t bit = w * pl.c;
@@ -139,14 +159,18 @@ __global__ void __launch_bounds__(MSM_THREADS)
       d -= (int32_t)(1u << pl.c);
       carry = 1;
     }
-    const size_t o = (size_t)w * n + i;
-    if (d == 0) {
-      keys[o] = sentinel;
-      vals[o] = 0;
-    } else {
-      const uint32_t mag = d < 0 ? (uint32_t)(-d) : (uint32_t)d;
-      keys[o] = w * pl.B + (mag - 1);
-      vals[o] = (uint32_t)i | (d < 0 ? 0x80000000u : 0u);
+    const uint32_t mag = d < 0 ? (uint32_t)(-d) : (uint32_t)d;
+    const uint32_t sign = d < 0 ? 0x80000000u : 0u;
+    for (uint32_t l = 0; l < g.n_lines; l++) {
+      const size_t o = ((size_t)w * g.n_lines + l) * m + j;
+      if (d == 0) {
+        keys[o] = sentinel;
+        vals[o] = 0;
+      } else {
+        const uint32_t grp = (l * g.n_chunks + chunk) * pl.W + w;
+        keys[o] = grp * pl.B + (mag - 1);
+        vals[o] = (uint32_t)(l * g.line_len + j) | sign;
+      }
     }
   }
 }
@@ -260,8 +284,8 @@ __global__ void __launch_bounds__(MSM_THREADS)
                       XYZZ<typename C::Fq>* __restrict__ partial) {
   using F = typename C::Fq;
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= pl.W * pl.T) return;
-  const uint32_t w = id / pl.T, sgm = id % pl.T;
+  if (id >= pl.G * pl.S) return;
+  const uint32_t w = id / pl.S, sgm = id % pl.S;
   const XYZZ<F>* bk = buckets + (size_t)w * pl.B + (size_t)sgm * pl.LS;
   XYZZ<F> run = xyzz_zero<F>(), acc = xyzz_zero<F>();
   for (int j = (int)pl.LS - 1; j >= 0; j--) {
@@ -274,7 +298,7 @@ __global__ void __launch_bounds__(MSM_THREADS)
 }
 
 // ---------------------------------------------------------------------------
-// 6. fold `cnt` consecutive points per window into ceil(cnt / MSM_FOLD)
+// 6. fold `cnt` consecutive points per group into ceil(cnt / MSM_FOLD)
 // ---------------------------------------------------------------------------
 template <class C>
 __global__ void __launch_bounds__(MSM_THREADS)
@@ -367,13 +391,120 @@ __global__ void __launch_bounds__(MSM_THREADS)
 }
 
 // ---------------------------------------------------------------------------
+// 7. batched form: per-task Horner fold over its W window sums + affine
+//    normalisation, one thread per task (the single-MSM path folds on the
+//    host instead, see msm_single_t).  Output: normalised Jacobian (x, y, 1)
+//    or (0, 1, 0), the reference's G::Curve layout (multiexp.cl:259-261
+//    writes one Jacobian per task).
+// ---------------------------------------------------------------------------
+template <class C>
+__global__ void __launch_bounds__(64)
+    msm_fold_kernel(const XYZZ<typename C::Fq>* __restrict__ sums, MsmPlan pl, uint32_t tasks,
+                    typename C::Fq* __restrict__ out) {
+  using F = typename C::Fq;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= tasks) return;
+  XYZZ<F> acc = xyzz_zero<F>();
+  for (int w = (int)pl.W - 1; w >= 0; w--) {
+    if (w != (int)pl.W - 1)
+      for (uint32_t k = 0; k < pl.c; k++) acc = xyzz_dbl<F, true>(acc);
+    acc = xyzz_add<F, true>(acc, load_xyzz(&sums[(size_t)t * pl.W + w]));
+  }
+  acc = xyzz_canon(acc);
+  const bool id = xyzz_is_zero(acc);
+  Jac<F> j = jac_from_affine_norm(xyzz_to_affine(acc), id);
+  store(&out[3 * (size_t)t], j.X);
+  store(&out[3 * (size_t)t + 1], j.Y);
+  store(&out[3 * (size_t)t + 2], j.Z);
+}
+
+// ---------------------------------------------------------------------------
 // host drivers
 // ---------------------------------------------------------------------------
 static inline uint32_t blocks_for(size_t n, int threads) { return (uint32_t)((n + threads - 1) / threads); }
 
+// Steps 1-6 for one device pass: leaves pl.G window sums (lazy XYZZ) on the
+// device and returns their address in *d_sums.
 template <class C>
-static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
-                     hipStream_t s, ecg_abort_cb abort_cb, void* user) {
+static int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
+                      const MsmPlan& pl, hipStream_t s, void** d_sums) {
+  using F = typename C::Fq;
+  using X = XYZZ<F>;
+  const size_t m = (size_t)g.n_chunks * g.clen;  // scalars consumed
+  const size_t total = (size_t)pl.W * g.n_lines * m;
+  const uint32_t nb = pl.G * pl.B;
+  const uint32_t sentinel = nb;
+  int key_bits = 1;
+  while ((1ull << key_bits) <= sentinel) key_bits++;
+  const size_t nseg = (total + pl.seg - 1) / pl.seg;
+
+  void *k0, *k1, *v0, *v1, *st, *en, *bk, *rc, *pa, *pb, *tmp;
+  ECG_TRY(ws_get(ctx, "msm_k0", total * 4, &k0));
+  ECG_TRY(ws_get(ctx, "msm_k1", total * 4, &k1));
+  ECG_TRY(ws_get(ctx, "msm_v0", total * 4, &v0));
+  ECG_TRY(ws_get(ctx, "msm_v1", total * 4, &v1));
+  ECG_TRY(ws_get(ctx, "msm_start", (size_t)nb * 4, &st));
+  ECG_TRY(ws_get(ctx, "msm_end", (size_t)nb * 4, &en));
+  ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nb * sizeof(X), &bk));
+  ECG_TRY(ws_get(ctx, "msm_recs", 2 * nseg * sizeof(X), &rc));
+  ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
+  ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * pl.S / MSM_FOLD + pl.G) * sizeof(X), &pb));
+
+  hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(m, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                     (const uint4*)d_scalars, g, pl, (uint32_t*)k0, (uint32_t*)v0);
+  ECG_HIP(hipGetLastError());
+
+  size_t tmp_bytes = 0;
+  ECG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
+                                             (uint32_t*)v1, total, 0, key_bits, s));
+  ECG_TRY(ws_get(ctx, "msm_sort_tmp", tmp_bytes, &tmp));
+  ECG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
+                                             (uint32_t*)v1, total, 0, key_bits, s));
+
+  ECG_HIP(hipMemsetAsync(st, 0, (size_t)nb * 4, s));
+  ECG_HIP(hipMemsetAsync(en, 0, (size_t)nb * 4, s));
+  hipLaunchKernelGGL(msm_bounds_kernel, dim3(blocks_for(total, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                     (const uint32_t*)k1, total, sentinel, (uint32_t*)st, (uint32_t*)en);
+  ECG_HIP(hipGetLastError());
+
+  ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
+  hipLaunchKernelGGL(msm_accumulate_kernel<C>, dim3(blocks_for(nseg, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                     (const F*)d_bases, (const uint32_t*)k1, (const uint32_t*)v1, total, sentinel, pl.seg,
+                     (const uint32_t*)st, (const uint32_t*)en, (X*)bk, (X*)rc);
+  ECG_HIP(hipGetLastError());
+  ECG_TRY(kt_end(ctx, "msm_accumulate", s));
+
+  hipLaunchKernelGGL(msm_fixup_kernel<C>, dim3(blocks_for(nb, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                     (const uint32_t*)k1, (const uint32_t*)st, (const uint32_t*)en, nb, pl.seg, (const X*)rc,
+                     (X*)bk);
+  ECG_HIP(hipGetLastError());
+
+  hipLaunchKernelGGL(msm_reduce_kernel<C>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
+                     dim3(MSM_THREADS), 0, s, (const X*)bk, pl, (X*)pa);
+  ECG_HIP(hipGetLastError());
+
+  uint32_t cnt = pl.S;
+  X* in = (X*)pa;
+  X* out = (X*)pb;
+  while (cnt > 1) {
+    const uint32_t oc = (cnt + MSM_FOLD - 1) / MSM_FOLD;
+    hipLaunchKernelGGL(msm_sum_kernel<C>, dim3(blocks_for((size_t)pl.G * oc, MSM_THREADS)), dim3(MSM_THREADS),
+                       0, s, (const X*)in, pl.G, cnt, oc, out);
+    ECG_HIP(hipGetLastError());
+    X* t = in;
+    in = out;
+    out = t;
+    cnt = oc;
+  }
+  *d_sums = in;
+  return ECG_OK;
+}
+
+// One MSM, processed in device passes of at most MSM_MAX_CHUNK terms; the
+// window sums come back to the host, which runs the Horner fold.
+template <class C>
+static int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
+                        hipStream_t s, ecg_abort_cb abort_cb, void* user) {
   using F = typename C::Fq;
   using X = XYZZ<F>;
   using HP = typename C::FqParams;
@@ -385,77 +516,12 @@ static int msm_run_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, s
     if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144
     const size_t m = n - off < MSM_MAX_CHUNK ? n - off : MSM_MAX_CHUNK;
     const MsmPlan pl = make_plan(m, (uint32_t)C::FrParams::BITS);
-    const size_t total = (size_t)pl.W * m;
-    const uint32_t nb = pl.W * pl.B;
-    const uint32_t sentinel = nb;
-    int key_bits = 1;
-    while ((1ull << key_bits) <= sentinel) key_bits++;
-    const size_t nseg = (total + pl.seg - 1) / pl.seg;
-
-    void *k0, *k1, *v0, *v1, *st, *en, *bk, *rc, *pa, *pb, *tmp;
-    ECG_TRY(ws_get(ctx, "msm_k0", total * 4, &k0));
-    ECG_TRY(ws_get(ctx, "msm_k1", total * 4, &k1));
-    ECG_TRY(ws_get(ctx, "msm_v0", total * 4, &v0));
-    ECG_TRY(ws_get(ctx, "msm_v1", total * 4, &v1));
-    ECG_TRY(ws_get(ctx, "msm_start", (size_t)nb * 4, &st));
-    ECG_TRY(ws_get(ctx, "msm_end", (size_t)nb * 4, &en));
-    ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nb * sizeof(X), &bk));
-    ECG_TRY(ws_get(ctx, "msm_recs", 2 * nseg * sizeof(X), &rc));
-    ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.W * pl.T * sizeof(X), &pa));
-    ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.W * pl.T / MSM_FOLD + pl.W) * sizeof(X), &pb));
-
-    const uint4* sc = (const uint4*)d_scalars + 2 * off;
-    const F* bases = (const F*)d_bases + 2 * off;
-
-    hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(m, MSM_THREADS)), dim3(MSM_THREADS), 0, s, sc, m, pl,
-                       (uint32_t*)k0, (uint32_t*)v0);
-    ECG_HIP(hipGetLastError());
-
-    size_t tmp_bytes = 0;
-    ECG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
-                                               (uint32_t*)v1, total, 0, key_bits, s));
-    ECG_TRY(ws_get(ctx, "msm_sort_tmp", tmp_bytes, &tmp));
-    ECG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
-                                               (uint32_t*)v1, total, 0, key_bits, s));
-
-    ECG_HIP(hipMemsetAsync(st, 0, (size_t)nb * 4, s));
-    ECG_HIP(hipMemsetAsync(en, 0, (size_t)nb * 4, s));
-    hipLaunchKernelGGL(msm_bounds_kernel, dim3(blocks_for(total, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                       (const uint32_t*)k1, total, sentinel, (uint32_t*)st, (uint32_t*)en);
-    ECG_HIP(hipGetLastError());
-
-    ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
-    hipLaunchKernelGGL(msm_accumulate_kernel<C>, dim3(blocks_for(nseg, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                       bases, (const uint32_t*)k1, (const uint32_t*)v1, total, sentinel, pl.seg, (const uint32_t*)st,
-                       (const uint32_t*)en, (X*)bk, (X*)rc);
-    ECG_HIP(hipGetLastError());
-    ECG_TRY(kt_end(ctx, "msm_accumulate", s));
-
-    hipLaunchKernelGGL(msm_fixup_kernel<C>, dim3(blocks_for(nb, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                       (const uint32_t*)k1, (const uint32_t*)st, (const uint32_t*)en, nb, pl.seg, (const X*)rc,
-                       (X*)bk);
-    ECG_HIP(hipGetLastError());
-
-    hipLaunchKernelGGL(msm_reduce_kernel<C>, dim3(blocks_for((size_t)pl.W * pl.T, MSM_THREADS)),
-                       dim3(MSM_THREADS), 0, s, (const X*)bk, pl, (X*)pa);
-    ECG_HIP(hipGetLastError());
-
-    uint32_t cnt = pl.T;
-    X* in = (X*)pa;
-    X* out = (X*)pb;
-    while (cnt > 1) {
-      const uint32_t oc = (cnt + MSM_FOLD - 1) / MSM_FOLD;
-      hipLaunchKernelGGL(msm_sum_kernel<C>, dim3(blocks_for((size_t)pl.W * oc, MSM_THREADS)), dim3(MSM_THREADS),
-                         0, s, (const X*)in, pl.W, cnt, oc, out);
-      ECG_HIP(hipGetLastError());
-      X* t = in;
-      in = out;
-      out = t;
-      cnt = oc;
-    }
+    const MsmGeom g{1, 1, m, m};
+    void* d_sums;
+    ECG_TRY(msm_core_t<C>(ctx, (const F*)d_bases + 2 * off, (const uint4*)d_scalars + 2 * off, g, pl, s, &d_sums));
     // window sums -> host; Horner fold over windows (multiexp.rs:221-233)
     win.resize(pl.W);
-    ECG_HIP(hipMemcpyAsync(win.data(), in, pl.W * sizeof(X), hipMemcpyDeviceToHost, s));
+    ECG_HIP(hipMemcpyAsync(win.data(), d_sums, pl.W * sizeof(X), hipMemcpyDeviceToHost, s));
     ECG_HIP(hipStreamSynchronize(s));
     HX acc = HX::zero();
     for (int w = (int)pl.W - 1; w >= 0; w--) {
@@ -485,10 +551,78 @@ int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scala
     return ECG_ERR_INVALID;
   }
   switch (curve_id) {
-    case ECG_CURVE_BLS12_381: return msm_run_t<BLS12_381>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user);
-    case ECG_CURVE_BN254: return msm_run_t<BN254>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user);
+    case ECG_CURVE_BLS12_381: return msm_single_t<BLS12_381>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user);
+    case ECG_CURVE_BN254: return msm_single_t<BN254>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user);
     default:
       set_error("multiexp: unknown curve_id %d", curve_id);
+      return ECG_ERR_INVALID;
+  }
+}
+
+// Batched multi-line MSM (ag-cuda-ec multiple_multiexp): all tasks in one
+// pass -- one sort over (task, window, bucket) keys, one accumulation launch,
+// one reduction -- then a device fold per task.  out_jac: tasks x 3 x Fq,
+// line-major (results[line * n_chunks + chunk], multiexp.cl:260).
+template <class C>
+static int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
+                       uint32_t window_bits, uint64_t* out_jac, hipStream_t s) {
+  using F = typename C::Fq;
+  kt_reset(ctx, "msm_accumulate");
+  const uint32_t tasks = g.tasks();
+  const size_t ob = (size_t)tasks * 3 * sizeof(F);
+  if (g.clen == 0) {  // empty chunks: every task is the identity
+    using HX = host::HXYZZ<typename C::FqParams>;
+    for (uint32_t t = 0; t < tasks; t++) host::hto_jac_norm(HX::zero(), out_jac + (size_t)t * 3 * C::FqParams::N);
+    return ECG_OK;
+  }
+  MsmPlan pl = make_plan(g.clen, (uint32_t)C::FrParams::BITS, window_bits);
+  pl.G = tasks * pl.W;
+  if ((uint64_t)pl.G * pl.B >= 0xffffffffull) {
+    set_error("multiple_multiexp: %u tasks x %u windows x %u buckets exceeds the 32-bit bucket space", tasks, pl.W,
+              pl.B);
+    return ECG_ERR_INVALID;
+  }
+  void *d_sums, *d_out;
+  ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums));
+  ECG_TRY(ws_get(ctx, "msm_batch_out", ob, &d_out));
+  hipLaunchKernelGGL(msm_fold_kernel<C>, dim3(blocks_for(tasks, 64)), dim3(64), 0, s, (const XYZZ<F>*)d_sums, pl,
+                     tasks, (F*)d_out);
+  ECG_HIP(hipGetLastError());
+  ECG_HIP(hipMemcpyAsync(out_jac, d_out, ob, hipMemcpyDeviceToHost, s));
+  ECG_HIP(hipStreamSynchronize(s));
+  return ECG_OK;
+}
+
+int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const void* d_scalars,
+                  size_t line_len, size_t n_chunks, uint32_t window_bits, uint64_t* out_jac, hipStream_t s) {
+  if (line_len == 0 || n_chunks == 0) {
+    set_error("multiple_multiexp: line_len and num_chunks must be positive");
+    return ECG_ERR_INVALID;
+  }
+  if (n_bases % line_len != 0) {
+    set_error("multiple_multiexp: %zu bases is not a whole number of lines of %zu", n_bases, line_len);
+    return ECG_ERR_INVALID;
+  }
+  if (n_bases > 0x7fffffffull) {
+    set_error("multiple_multiexp: at most 2^31-1 bases per call");
+    return ECG_ERR_INVALID;
+  }
+  if (window_bits > 22) {
+    set_error("multiple_multiexp: window_size %u out of range [0, 22] (0 = automatic)", window_bits);
+    return ECG_ERR_INVALID;
+  }
+  const size_t n_lines = n_bases / line_len;
+  if (n_lines == 0) return ECG_OK;
+  if (n_lines * n_chunks > 0xffffffull) {
+    set_error("multiple_multiexp: %zu tasks is too many", n_lines * n_chunks);
+    return ECG_ERR_INVALID;
+  }
+  const MsmGeom g{(uint32_t)n_lines, (uint32_t)n_chunks, line_len, line_len / n_chunks};
+  switch (curve_id) {
+    case ECG_CURVE_BLS12_381: return msm_batch_t<BLS12_381>(ctx, d_bases, d_scalars, g, window_bits, out_jac, s);
+    case ECG_CURVE_BN254: return msm_batch_t<BN254>(ctx, d_bases, d_scalars, g, window_bits, out_jac, s);
+    default:
+      set_error("multiple_multiexp: unknown curve_id %d", curve_id);
       return ECG_ERR_INVALID;
   }
 }

@@ -86,6 +86,9 @@ _SIGS = {
     "ecg_point_sum_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, _u64p,
                                          ctypes.c_void_p]),
     "ecg_point_sum": (ctypes.c_int, [ctypes.c_int, _u64p, ctypes.c_size_t, _u64p]),
+    "ecg_multiple_multiexp": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
+                                             ctypes.c_uint32, _u64p]),
     "ecg_msm_check_bases": (ctypes.c_int, [ctypes.c_int, _u64p, _u64p, ctypes.c_size_t]),
     "ecg_gen_bases_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, ctypes.c_size_t,
                                          ctypes.c_void_p, ctypes.c_void_p]),
@@ -342,6 +345,51 @@ def gen_bases_dev(prog: Program, curve, a: int, b: int, n: int) -> DeviceBuffer:
     bu = np.array([(b >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
     _check(lib().ecg_gen_bases_dev(prog.handle, cid, _ptr(au), _ptr(bu), n, buf.ptr, None), "gen_bases")
     return buf
+
+
+# ---------------------------------------------------------------------------
+# ag-cuda-ec batched multi-line MSM (ag-cuda-ec/src/multiexp.rs)
+# ---------------------------------------------------------------------------
+
+
+def upload_multiexp_bases(prog: Program, bases: np.ndarray) -> DeviceBuffer:
+    """ag_cuda_ec::multiexp::upload_multiexp_bases (multiexp.rs:11-19): affine
+    bases (n, 2*Lq) u64, Montgomery x||y, identity = zeros (GpuRepr) -> HBM."""
+    return DeviceBuffer.upload(prog, np.ascontiguousarray(bases, dtype=np.uint64))
+
+
+def multiple_multiexp(prog: Program, bases_gpu: DeviceBuffer, exponents, num_chunks: int,
+                      window_size: int = 0, neg_is_cheap: bool = True, curve="bls12_381",
+                      pin_window: bool = False) -> np.ndarray:
+    """ag_cuda_ec::multiexp::multiple_multiexp (multiexp.rs:21-81).
+
+    bases_gpu holds n_lines * len(exponents) bases; `exponents` is one row of
+    canonical scalars ((line_len, 4) u64 host array, or a DeviceBuffer plus
+    line_len via a (buffer, line_len) tuple).  Returns (n_lines * num_chunks,
+    3*Lq) normalised Jacobian points, result[line * num_chunks + chunk].
+    window_size / neg_is_cheap are the reference kernel's tuning knobs; results
+    never depend on them.  The engine picks its own window unless
+    pin_window=True (then window_size in 1..22 is used as is)."""
+    cid = _curve(curve)
+    lq = CURVE_FQ_LIMBS[cid]
+    if isinstance(exponents, tuple):
+        dbuf, line_len = exponents
+        sc_ptr, on_dev = dbuf.ptr, 1
+        keep = None
+    else:
+        keep = np.ascontiguousarray(exponents, dtype=np.uint64).reshape(-1, 4)
+        line_len = keep.shape[0]
+        sc_ptr, on_dev = keep.ctypes.data_as(ctypes.c_void_p), 0
+    if line_len == 0:
+        raise EcError("multiple_multiexp: empty exponent row")
+    n_bases = bases_gpu.nbytes // (2 * lq * 8)
+    n_lines = n_bases // line_len
+    out = np.zeros((n_lines * num_chunks, 3 * lq), dtype=np.uint64)
+    wb = int(window_size) if pin_window else 0
+    _check(lib().ecg_multiple_multiexp(prog.handle, cid, bases_gpu.ptr, n_lines * line_len, sc_ptr, on_dev,
+                                       line_len, num_chunks, wb, _ptr(out)), "multiple_multiexp")
+    del keep
+    return out
 
 
 def program(device: Device) -> Program:

@@ -118,6 +118,23 @@ int ecg_msm_multi(ecg_ctx **ctxs, int nctx, int curve_id, const uint64_t *bases_
 int ecg_msm_dev(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n,
                 void *out_jac, int out_on_device, void *stream);
 
+/* Batched multi-line MSM: ag_cuda_ec::multiexp::multiple_multiexp
+ * (ag-cuda-ec/src/multiexp.rs:21-81; kernel ag-build/cl/multiexp.cl:215-262).
+ * d_bases holds n_bases affine points (x, y Montgomery, identity = zeros) as
+ * uploaded by upload_multiexp_bases (multiexp.rs:11-19), i.e. n_bases /
+ * line_len lines of line_len bases; `scalars` is ONE row of line_len canonical
+ * scalars (4 x u64 each) shared by every line -- host memory, or device memory
+ * with scalars_on_device != 0.  Each line is split into num_chunks chunks of
+ * line_len / num_chunks terms (a remainder is ignored, as the reference's
+ * kernel does) and out_jac[line * num_chunks + chunk] (3 x Lq u64, host
+ * memory, normalised Jacobian) receives that chunk's MSM.  window_bits = 0
+ * lets the engine choose the window; 1..22 pins it (the reference's
+ * window_size; results never depend on it).  The reference's neg_is_cheap
+ * flag has no analogue: digits are always signed. */
+int ecg_multiple_multiexp(ecg_ctx *ctx, int curve_id, const void *d_bases, size_t n_bases,
+                          const uint64_t *scalars, int scalars_on_device, size_t line_len,
+                          size_t num_chunks, uint32_t window_bits, uint64_t *out_jac);
+
 /* Sum `count` Jacobian points (3 x Lq u64 each, device memory) into one
  * normalised Jacobian point: the EC fold that follows the RCCL all-gather of
  * per-GPU partials (RCCL has no EC-add reduction op).  out is host memory. */
