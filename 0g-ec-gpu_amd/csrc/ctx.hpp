@@ -93,6 +93,9 @@ int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scala
             uint64_t* out_jac, hipStream_t s, ecg_abort_cb abort_cb, void* user);
 int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, uint64_t* out_jac,
                   hipStream_t s);
+int ecfft_validate(int curve_id, uint32_t log_n);
+int ecfft_run(ecg_ctx* ctx, int curve_id, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
+              ecg_abort_cb abort_cb, void* user);
 int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const void* d_scalars,
                   size_t line_len, size_t n_chunks, uint32_t window_bits, uint64_t* out_jac, hipStream_t s);
 int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac);

@@ -215,6 +215,21 @@ ECG_DEV XYZZ<F> xyzz_mul_small(const XYZZ<F>& p, uint32_t k) {
   return acc;
 }
 
+// k * P for a canonical multi-word scalar k (8 x u32, little-endian),
+// double-and-add from the top set bit.
+template <class F, bool LZ = false>
+ECG_DEV XYZZ<F> xyzz_mul_scalar(const XYZZ<F>& p, const uint32_t* k) {
+  int top = 255;
+  while (top >= 0 && !((k[top >> 5] >> (top & 31)) & 1)) top--;
+  if (top < 0 || xyzz_is_zero<F, LZ>(p)) return xyzz_zero<F>();
+  XYZZ<F> acc = p;
+  for (int b = top - 1; b >= 0; b--) {
+    acc = xyzz_dbl<F, LZ>(acc);
+    if ((k[b >> 5] >> (b & 31)) & 1) acc = xyzz_add<F, LZ>(acc, p);
+  }
+  return acc;
+}
+
 // Canonicalise every coordinate (lazy [0, 2p] -> [0, p)).
 template <class F>
 ECG_DEV XYZZ<F> xyzz_canon(const XYZZ<F>& p) {

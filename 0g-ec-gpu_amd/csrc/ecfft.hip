@@ -1,0 +1,159 @@
+// FFT over G1 ("EC-FFT", FFTg) for gfx950:  out_k = sum_j omega^(jk) * P_j.
+//
+// Replaces SingleEcFftKernel::radix_ec_fft (ec-gpu-proxy/src/ec_fft.rs:56-164),
+// ag_cuda_ec::ec_fft::radix_ec_fft (ag-cuda-ec/src/ec_fft.rs:12-93) and their
+// kernel POINT_radix_fft (ag-build/cl/ec-fft.cl:4-70).  Semantics follow
+// serial_ec_fft (ec-gpu-proxy/src/ec_fft_cpu.rs:12-56): natural-order in and
+// out, omega a primitive 2^log_n-th root of unity of Fr.
+//
+// Re-design.  A butterfly here is one full scalar
+// multiplication (~255 doublings + ~128 adds, thousands of Fq products) on
+// ~200 bytes of point data: the transform is VALU-bound by three orders of
+// magnitude over its HBM traffic, so the Stockham/LDS staging that the scalar
+// NTT needs buys nothing.  The layout is instead the one that maximises
+// independent lanes per launch:
+//   1. ecfft_load      Jacobian (any Z) -> XYZZ, written to bit-reversed slots
+//   2. ecfft_twiddle   omega^i, i < n/2, canonical (scalar-mul bit source)
+//   3. ecfft_stage     log_n launches of n/2 independent radix-2 DIT
+//                      butterflies (A, B) -> (A + wB, A - wB), lazy [0, 2p]
+//                      Fq arithmetic, w = 1 butterflies skip the multiply
+//   4. ecfft_store     XYZZ -> normalised Jacobian (x, y, 1) / (0, 1, 0)
+#include <cstring>
+
+#include "ctx.hpp"
+#include "curve.hpp"
+
+namespace ecg {
+
+constexpr int ECFFT_THREADS = 64;
+
+template <class C>
+__global__ void __launch_bounds__(ECFFT_THREADS)
+    ecfft_load_kernel(const typename C::Fq* __restrict__ jac, uint32_t log_n, XYZZ<typename C::Fq>* __restrict__ a) {
+  using F = typename C::Fq;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (1u << log_n)) return;
+  Jac<F> j;
+  j.X = load(&jac[3 * (size_t)i]);
+  j.Y = load(&jac[3 * (size_t)i + 1]);
+  j.Z = load(&jac[3 * (size_t)i + 2]);
+  const uint32_t r = log_n ? (__brev(i) >> (32 - log_n)) : 0u;
+  store_xyzz(&a[r], xyzz_from_jac(j));
+}
+
+template <class C>
+__global__ void __launch_bounds__(ECFFT_THREADS)
+    ecfft_twiddle_kernel(Fp<typename C::FrParams> omega, uint32_t half, uint4* __restrict__ tw) {
+  using S = Fp<typename C::FrParams>;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= half) return;
+  S w = from_mont(fpow_u32(omega, i));
+  tw[2 * i] = make_uint4(w.v[0], w.v[1], w.v[2], w.v[3]);
+  tw[2 * i + 1] = make_uint4(w.v[4], w.v[5], w.v[6], w.v[7]);
+}
+
+// Stage s of the DIT: half-size h = 2^s; butterfly t pairs i0 = (t >> s) *
+// 2h + j and i1 = i0 + h, j = t mod h, twiddle omega^(j * n / 2h)
+// (serial_ec_fft's w = w_m^j, ec_fft_cpu.rs:35-49).
+template <class C>
+__global__ void __launch_bounds__(ECFFT_THREADS)
+    ecfft_stage_kernel(XYZZ<typename C::Fq>* __restrict__ a, const uint4* __restrict__ tw, uint32_t log_n,
+                       uint32_t s) {
+  using F = typename C::Fq;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (1u << (log_n - 1))) return;
+  const uint32_t h = 1u << s;
+  const uint32_t j = t & (h - 1);
+  const uint32_t i0 = ((t >> s) << (s + 1)) + j, i1 = i0 + h;
+  XYZZ<F> A = load_xyzz(&a[i0]);
+  XYZZ<F> B = load_xyzz(&a[i1]);
+  if (j != 0) {
+    const uint32_t e = j << (log_n - 1 - s);
+    const uint4 lo = tw[2 * e], hi = tw[2 * e + 1];
+    const uint32_t k[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    B = xyzz_mul_scalar<F, true>(B, k);
+  }
+  store_xyzz(&a[i0], xyzz_add<F, true>(A, B));
+  store_xyzz(&a[i1], xyzz_add<F, true>(A, xyzz_neg<F, true>(B)));
+}
+
+template <class C>
+__global__ void __launch_bounds__(ECFFT_THREADS)
+    ecfft_store_kernel(const XYZZ<typename C::Fq>* __restrict__ a, uint32_t n, typename C::Fq* __restrict__ jac) {
+  using F = typename C::Fq;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  XYZZ<F> p = xyzz_canon(load_xyzz(&a[i]));
+  const bool id = xyzz_is_zero(p);
+  Jac<F> j = jac_from_affine_norm(xyzz_to_affine(p), id);
+  store(&jac[3 * (size_t)i], j.X);
+  store(&jac[3 * (size_t)i + 1], j.Y);
+  store(&jac[3 * (size_t)i + 2], j.Z);
+}
+
+static inline uint32_t ecfft_blocks(size_t n) { return (uint32_t)((n + ECFFT_THREADS - 1) / ECFFT_THREADS); }
+
+template <class C>
+static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
+                   ecg_abort_cb abort_cb, void* user) {
+  using F = typename C::Fq;
+  using S = Fp<typename C::FrParams>;
+  const uint32_t n = 1u << log_n;
+  void *a, *tw;
+  ECG_TRY(ws_get(ctx, "ecfft_pts", (size_t)n * sizeof(XYZZ<F>), &a));
+  ECG_TRY(ws_get(ctx, "ecfft_tw", (size_t)(n / 2 + 1) * 32, &tw));
+  S om;
+  memcpy(om.v, omega, sizeof(om.v));
+  hipLaunchKernelGGL(ecfft_load_kernel<C>, dim3(ecfft_blocks(n)), dim3(ECFFT_THREADS), 0, s, (const F*)d_jac, log_n,
+                     (XYZZ<F>*)a);
+  ECG_HIP(hipGetLastError());
+  if (log_n > 0) {
+    hipLaunchKernelGGL(ecfft_twiddle_kernel<C>, dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s, om, n / 2,
+                       (uint4*)tw);
+    ECG_HIP(hipGetLastError());
+  }
+  kt_reset(ctx, "ecfft_stage");
+  for (uint32_t st = 0; st < log_n; st++) {
+    if (abort_cb && abort_cb(user)) {  // ec_fft.rs:112-116, once per round
+      (void)hipStreamSynchronize(s);
+      return ECG_ABORTED;
+    }
+    ECG_TRY(kt_begin(ctx, "ecfft_stage", s));
+    hipLaunchKernelGGL(ecfft_stage_kernel<C>, dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s, (XYZZ<F>*)a,
+                       (const uint4*)tw, log_n, st);
+    ECG_HIP(hipGetLastError());
+    ECG_TRY(kt_end(ctx, "ecfft_stage", s));
+  }
+  hipLaunchKernelGGL(ecfft_store_kernel<C>, dim3(ecfft_blocks(n)), dim3(ECFFT_THREADS), 0, s, (const XYZZ<F>*)a, n,
+                     (F*)d_jac);
+  ECG_HIP(hipGetLastError());
+  return ECG_OK;
+}
+
+int ecfft_validate(int curve_id, uint32_t log_n) {
+  uint32_t two_adicity;
+  switch (curve_id) {
+    case ECG_CURVE_BLS12_381: two_adicity = BLS12_381::FrParams::TWO_ADICITY; break;
+    case ECG_CURVE_BN254: two_adicity = BN254::FrParams::TWO_ADICITY; break;
+    default:
+      set_error("ec_fft: unknown curve_id %d", curve_id);
+      return ECG_ERR_INVALID;
+  }
+  // ec_fft.rs:13 LOG2_MAX_ELEMENTS = 32; the Fr two-adicity bounds it further.
+  if (log_n > two_adicity || log_n > 31) {
+    set_error("ec_fft: log_n = %u exceeds the supported maximum (two-adicity %u, 2^31 points)", log_n, two_adicity);
+    return ECG_ERR_INVALID;
+  }
+  return ECG_OK;
+}
+
+int ecfft_run(ecg_ctx* ctx, int curve_id, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
+              ecg_abort_cb abort_cb, void* user) {
+  ECG_TRY(ecfft_validate(curve_id, log_n));
+  switch (curve_id) {
+    case ECG_CURVE_BLS12_381: return ecfft_t<BLS12_381>(ctx, d_jac, omega, log_n, s, abort_cb, user);
+    default: return ecfft_t<BN254>(ctx, d_jac, omega, log_n, s, abort_cb, user);
+  }
+}
+
+}  // namespace ecg

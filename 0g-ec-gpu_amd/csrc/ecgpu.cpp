@@ -286,6 +286,77 @@ int ecg_fft_many(ecg_ctx** ctxs, int nctx, int field_id, uint64_t** inouts, cons
   return first_err.load();
 }
 
+// ---------------------------------------------------------------- EC-FFT
+int ecg_ec_fft(ecg_ctx* ctx, int curve_id, uint64_t* inout_jac, const uint64_t* omega, uint32_t log_n,
+               ecg_abort_cb abort_cb, void* user) {
+  ECG_TRY(ctx_enter(ctx));
+  if (!inout_jac || !omega) {
+    set_error("ecg_ec_fft: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  ECG_TRY(ecfft_validate(curve_id, log_n));  // before any allocation or copy
+  const size_t bytes = ((size_t)1 << log_n) * 3 * fq_limbs64(curve_id) * 8;
+  void* d;
+  ECG_TRY(ws_get(ctx, "ecfft_io", bytes, &d));
+  hipStream_t s = ctx->stream;
+  ECG_HIP(hipMemcpyAsync(d, inout_jac, bytes, hipMemcpyHostToDevice, s));  // ec_fft.rs:103
+  int rc = ecfft_run(ctx, curve_id, d, omega, log_n, s, abort_cb, user);
+  if (rc != ECG_OK) {
+    (void)hipStreamSynchronize(s);
+    return rc;
+  }
+  ECG_HIP(hipMemcpyAsync(inout_jac, d, bytes, hipMemcpyDeviceToHost, s));  // ec_fft.rs:158
+  ECG_HIP(hipStreamSynchronize(s));
+  return kt_collect(ctx);
+}
+
+int ecg_ec_fft_dev(ecg_ctx* ctx, int curve_id, void* d_inout_jac, const uint64_t* omega, uint32_t log_n,
+                   void* stream) {
+  ECG_TRY(ctx_enter(ctx));
+  if (!d_inout_jac || !omega) {
+    set_error("ecg_ec_fft_dev: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  hipStream_t s = pick_stream(ctx, stream);
+  ECG_TRY(ecfft_run(ctx, curve_id, d_inout_jac, omega, log_n, s, nullptr, nullptr));
+  ECG_HIP(hipStreamSynchronize(s));
+  return kt_collect(ctx);
+}
+
+int ecg_ec_fft_many(ecg_ctx** ctxs, int nctx, int curve_id, uint64_t** inouts, const uint64_t* omegas,
+                    const uint32_t* log_ns, size_t count, ecg_abort_cb abort_cb, void* user) {
+  if (!ctxs || nctx <= 0) {
+    set_error("No working GPUs found!");  // ec_fft.rs:207
+    return ECG_ERR_NODEV;
+  }
+  if (count == 0) return ECG_OK;
+  const size_t chunk = (count + nctx - 1) / nctx;  // ec_fft.rs:231
+  std::atomic<int> first_err{ECG_OK};
+  std::mutex mu;
+  std::string err_msg;
+  std::vector<std::thread> th;
+  for (int d = 0; d < nctx && (size_t)d * chunk < count; d++) {
+    th.emplace_back([&, d]() {
+      const size_t i0 = d * chunk, i1 = std::min(count, i0 + chunk);
+      for (size_t i = i0; i < i1; i++) {
+        if (first_err.load() != ECG_OK) break;  // ec_fft.rs:249-251
+        int rc = ecg_ec_fft(ctxs[d], curve_id, inouts[i], omegas + 4 * i, log_ns[i], abort_cb, user);
+        if (rc != ECG_OK) {
+          int expected = ECG_OK;
+          if (first_err.compare_exchange_strong(expected, rc)) {
+            std::lock_guard<std::mutex> g(mu);
+            err_msg = g_err;
+          }
+          break;
+        }
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  if (first_err.load() != ECG_OK) g_err = err_msg;
+  return first_err.load();
+}
+
 // ---------------------------------------------------------------- MSM
 static int msm_host(ecg_ctx* ctx, int curve_id, const uint64_t* bases_xy, const uint64_t* scalars, size_t n,
                     uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {

@@ -86,6 +86,13 @@ _SIGS = {
     "ecg_point_sum_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, _u64p,
                                          ctypes.c_void_p]),
     "ecg_point_sum": (ctypes.c_int, [ctypes.c_int, _u64p, ctypes.c_size_t, _u64p]),
+    "ecg_ec_fft": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, ctypes.c_uint32, ABORT_CB,
+                                  ctypes.c_void_p]),
+    "ecg_ec_fft_many": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(_u64p), _u64p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t,
+                                       ABORT_CB, ctypes.c_void_p]),
+    "ecg_ec_fft_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, _u64p, ctypes.c_uint32,
+                                      ctypes.c_void_p]),
     "ecg_multiple_multiexp": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                              ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
                                              ctypes.c_uint32, _u64p]),
@@ -213,8 +220,9 @@ def generate(sb: SourceBuilder) -> None:
     for c in sb.multiexps:
         if c not in CURVE_NAMES:
             raise EcError(f"no prebuilt multiexp for curve {c!r}")
-    if sb.ec_ffts:
-        raise EcError("G1 EC-FFT (add_ec_fft) is not part of this build (SURVEY §8f next #2)")
+    for c in sb.ec_ffts:
+        if c not in CURVE_NAMES:
+            raise EcError(f"no prebuilt EC-FFT for curve {c!r}")
     lib()
 
 
@@ -477,6 +485,101 @@ class FftKernel:
         rc = lib().ecg_fft_many(ctxs, nd, self.kernels[0].fid, ptrs, _ptr(om), lns, n, cb, None)
         del keep
         _check(rc, "radix_fft_many")
+
+
+# ---------------------------------------------------------------------------
+# EC-FFT over G1 (ec-gpu-proxy/src/ec_fft.rs, ag-cuda-ec/src/ec_fft.rs)
+# ---------------------------------------------------------------------------
+
+
+def _jac_shape(cid: int, log_n: int):
+    return (1 << log_n, 3 * CURVE_FQ_LIMBS[cid])
+
+
+class SingleEcFftKernel:
+    def __init__(self, prog: Program, cid: int, maybe_abort=None):
+        self.program = prog
+        self.cid = cid
+        self.maybe_abort = maybe_abort
+
+    def radix_ec_fft(self, inp: np.ndarray, omega: np.ndarray, log_n: int) -> None:
+        """In place (ec_fft.rs:56-164): inp (2^log_n, 3*Lq) uint64 Jacobian points
+        (G::Curve, Montgomery), rewritten normalised; omega Fr Montgomery."""
+        if inp.shape != _jac_shape(self.cid, log_n) or inp.dtype != np.uint64 or not inp.flags["C_CONTIGUOUS"]:
+            raise EcError(f"radix_ec_fft: expected a C-contiguous uint64 array of shape {_jac_shape(self.cid, log_n)}")
+        om = np.ascontiguousarray(omega, dtype=np.uint64).reshape(4)
+        cb, keep = _abort_cb(self.maybe_abort)
+        with self.program._lock:
+            rc = lib().ecg_ec_fft(self.program.handle, self.cid, _ptr(inp), _ptr(om), log_n, cb, None)
+        del keep
+        _check(rc, "radix_ec_fft")
+
+
+class EcFftKernel:
+    """One EC-FFT kernel per device (ec_fft.rs:167-271)."""
+
+    def __init__(self, kernels: list[SingleEcFftKernel]):
+        self.kernels = kernels
+
+    @staticmethod
+    def create(programs: Sequence[Program], curve: str | int = "bls12_381") -> "EcFftKernel":
+        return EcFftKernel._create(programs, curve, None)
+
+    @staticmethod
+    def create_with_abort(programs, maybe_abort: Callable[[], bool], curve: str | int = "bls12_381"):
+        return EcFftKernel._create(programs, curve, maybe_abort)
+
+    @staticmethod
+    def _create(programs, curve, maybe_abort):
+        cid = _curve(curve)
+        kernels = [SingleEcFftKernel(p, cid, maybe_abort) for p in programs]
+        if not kernels:
+            raise EcError("No working GPUs found!")
+        return EcFftKernel(kernels)
+
+    def radix_ec_fft(self, inp: np.ndarray, omega: np.ndarray, log_n: int) -> None:
+        """Uses the first GPU (ec_fft.rs:213-217)."""
+        self.kernels[0].radix_ec_fft(inp, omega, log_n)
+
+    def radix_ec_fft_many(self, inputs: Sequence[np.ndarray], omegas: Sequence[np.ndarray],
+                          log_ns: Sequence[int]) -> None:
+        """ceil(m / #devices) transforms per device, first error wins (ec_fft.rs:224-270)."""
+        n = len(inputs)
+        if not (len(omegas) == n and len(log_ns) == n):
+            raise EcError("radix_ec_fft_many: inputs/omegas/log_ns length mismatch")
+        if n == 0:
+            return
+        cid = self.kernels[0].cid
+        for a, ln in zip(inputs, log_ns):
+            if a.shape != _jac_shape(cid, ln) or a.dtype != np.uint64 or not a.flags["C_CONTIGUOUS"]:
+                raise EcError("radix_ec_fft_many: each input must be a C-contiguous (2^log_n, 3*Lq) uint64 array")
+        nd = len(self.kernels)
+        ctxs = (ctypes.c_void_p * nd)(*[k.program.handle.value for k in self.kernels])
+        ptrs = (_u64p * n)(*[_ptr(a) for a in inputs])
+        om = np.ascontiguousarray(np.stack([np.asarray(o, dtype=np.uint64).reshape(4) for o in omegas]))
+        lns = (ctypes.c_uint32 * n)(*log_ns)
+        cb, keep = _abort_cb(self.kernels[0].maybe_abort)
+        rc = lib().ecg_ec_fft_many(ctxs, nd, cid, ptrs, _ptr(om), lns, n, cb, None)
+        del keep
+        _check(rc, "radix_ec_fft_many")
+
+
+def radix_ec_fft(prog: Program, inp: np.ndarray, omegas, curve="bls12_381") -> None:
+    """ag_cuda_ec::ec_fft::radix_ec_fft (ag-cuda-ec/src/ec_fft.rs:12-93): in
+    place, n = len(inp) a power of two; omegas[0] is the n-th root of unity
+    (the reference passes [omega, omega^2, omega^4, ...])."""
+    n = inp.shape[0]
+    log_n = n.bit_length() - 1
+    if n != 1 << log_n:
+        raise EcError("radix_ec_fft: input length must be a power of two")
+    SingleEcFftKernel(prog, _curve(curve)).radix_ec_fft(inp, np.asarray(omegas, dtype=np.uint64).reshape(-1, 4)[0],
+                                                        log_n)
+
+
+def ec_fft_dev(prog: Program, curve, d_data: DeviceBuffer, omega: np.ndarray, log_n: int) -> None:
+    """In-place EC-FFT of HBM-resident Jacobian points (ecg_ec_fft_dev)."""
+    om = np.ascontiguousarray(omega, dtype=np.uint64).reshape(4)
+    _check(lib().ecg_ec_fft_dev(prog.handle, _curve(curve), d_data.ptr, _ptr(om), log_n, None), "ec_fft_dev")
 
 
 # ---------------------------------------------------------------------------

@@ -93,6 +93,25 @@ int ecg_fft_many(ecg_ctx **ctxs, int nctx, int field_id, uint64_t **inouts, cons
 int ecg_fft_dev(ecg_ctx *ctx, int field_id, void *d_inout, const uint64_t *omega, uint32_t log_n,
                 void *stream);
 
+/* ---- EC-FFT (FFT over G1, "FFTg") -------------------------------------------
+ * In-place DFT of 2^log_n G1 points: P_k <- sum_j omega^(j k) * P_j, natural
+ * order in and out, omega an Fr element (Montgomery, 4 x u64) that is a
+ * primitive 2^log_n-th root of unity.  inout: 2^log_n Jacobian points
+ * (3 x Lq u64 each, any Z; Z = 0 is the identity), rewritten normalised.
+ * Replaces SingleEcFftKernel::radix_ec_fft (ec-gpu-proxy/src/ec_fft.rs:56-164)
+ * and ag_cuda_ec::ec_fft::radix_ec_fft (ag-cuda-ec/src/ec_fft.rs:12-93);
+ * result == serial_ec_fft (ec_fft_cpu.rs:12-56).  log_n <= min(31, Fr
+ * two-adicity); log_n = 0 returns the (normalised) input. */
+int ecg_ec_fft(ecg_ctx *ctx, int curve_id, uint64_t *inout_jac, const uint64_t *omega, uint32_t log_n,
+               ecg_abort_cb abort_cb, void *user);
+/* EcFftKernel::radix_ec_fft_many (ec_fft.rs:224-270): ceil(count / nctx)
+ * transforms per context, one host thread per context, first error wins. */
+int ecg_ec_fft_many(ecg_ctx **ctxs, int nctx, int curve_id, uint64_t **inouts, const uint64_t *omegas,
+                    const uint32_t *log_ns, size_t count, ecg_abort_cb abort_cb, void *user);
+/* Device-resident variant (d_inout_jac on ctx's device). */
+int ecg_ec_fft_dev(ecg_ctx *ctx, int curve_id, void *d_inout_jac, const uint64_t *omega, uint32_t log_n,
+                   void *stream);
+
 /* ---- MSM ------------------------------------------------------------------
  * out = sum_{i<n} scalars[i] * bases[i] on curve_id's G1.
  * Replaces SingleMultiexpKernel::multiexp (ec-gpu-proxy/src/multiexp.rs:135-236)

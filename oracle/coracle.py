@@ -57,6 +57,8 @@ def lib():
             "orc_gen_mul": (None, [i, _u64p, _u64p]),
             "orc_gen_bases": (None, [i, _u64p, _u64p, sz, _u64p, i]),
             "orc_kat_scalar": (None, [i, _u64p, _u64p, _u64p, sz, _u64p, i]),
+            "orc_serial_ec_fft": (None, [i, _u64p, _u64p, u32, i]),
+            "orc_naive_ec_dft": (None, [i, _u64p, _u64p, u32, _u64p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -173,3 +175,17 @@ def kat_scalar(cid: int, a: int, b: int, scalars: np.ndarray, nthreads: int = 8)
     lib().orc_kat_scalar(cid, ptr(u64arr([a], 4)[0]), ptr(u64arr([b], 4)[0]), ptr(sc), sc.size // 4,
                          ptr(out), nthreads)
     return to_ints(out.reshape(1, 4))[0]
+
+
+def serial_ec_fft(cid: int, pts: np.ndarray, omega: np.ndarray, log_n: int, nthreads: int = 8) -> np.ndarray:
+    """serial_ec_fft (ec_fft_cpu.rs:12-56) on (n, 3*Lq) Jacobian points; returns a copy."""
+    a = np.array(pts, dtype=np.uint64, order="C", copy=True)
+    lib().orc_serial_ec_fft(cid, ptr(a), ptr(np.ascontiguousarray(omega, dtype=np.uint64)), log_n, nthreads)
+    return a
+
+
+def naive_ec_dft(cid: int, pts: np.ndarray, omega: np.ndarray, log_n: int) -> np.ndarray:
+    a = np.ascontiguousarray(pts, dtype=np.uint64)
+    out = np.zeros_like(a)
+    lib().orc_naive_ec_dft(cid, ptr(a), ptr(np.ascontiguousarray(omega, dtype=np.uint64)), log_n, ptr(out))
+    return out

@@ -87,8 +87,9 @@ def test_source_builder_and_generate():
     ecgpu.generate(sb)
     with pytest.raises(ecgpu.EcError):
         ecgpu.generate(ecgpu.SourceBuilder.new().add_fft("bls12_381_fq"))
+    ecgpu.generate(ecgpu.SourceBuilder.new().add_ec_fft("bls12_381").add_ec_fft("bn254"))
     with pytest.raises(ecgpu.EcError):
-        ecgpu.generate(ecgpu.SourceBuilder.new().add_ec_fft("bls12_381"))
+        ecgpu.generate(ecgpu.SourceBuilder.new().add_ec_fft("bls12_377"))
 
 
 def test_worker_threads_env(monkeypatch):
