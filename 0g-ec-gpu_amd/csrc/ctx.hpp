@@ -59,6 +59,17 @@ struct ecg_ctx {
   int tw_variant = 0;
   uint32_t tw_log_n = 0;
   uint64_t tw_omega[4] = {0, 0, 0, 0};
+  // persistent base cache: converted [x, y] bases keyed by the
+  // caller's host buffer, reused while the same (pointer, size, curve,
+  // layout) comes back -- the reference's Arc<Vec<G>> bases are immutable.
+  struct BaseCache {
+    const void* host = nullptr;
+    size_t n = 0;
+    int curve = -1;
+    int layout = -1;
+    void* dev = nullptr;
+  };
+  std::vector<BaseCache> base_cache;
   // kernel timing (HIP events on the launch stream)
   std::map<std::string, ecg::KernelTimes> ktimes;
   std::vector<hipEvent_t> event_pool;
@@ -89,15 +100,22 @@ int ntt_run(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uin
             hipStream_t s, ecg_abort_cb abort_cb, void* user);
 // MSM / point-sum results are written to HOST memory (3 x Lq u64, normalised
 // Jacobian): the last serial steps (window fold, normalisation) run on the host.
+// scalar_mont: scalars are Montgomery Fr elements (converted on device).
 int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n,
-            uint64_t* out_jac, hipStream_t s, ecg_abort_cb abort_cb, void* user);
+            uint64_t* out_jac, hipStream_t s, ecg_abort_cb abort_cb, void* user, int scalar_mont = 0);
+// Host-side prep moved on device (prep.hip): density compaction of exps
+// (DensityTracker::generate_exps), ark Affine{x,y,infinity} -> [x,y].
+int density_compact(ecg_ctx* ctx, const void* d_exps, const uint64_t* d_bits, size_t n, void* d_out,
+                    size_t* out_count, hipStream_t s);
+int bases_from_ark(ecg_ctx* ctx, int curve_id, const void* d_ark, size_t n, void* d_xy, hipStream_t s);
 int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, uint64_t* out_jac,
                   hipStream_t s);
 int ecfft_validate(int curve_id, uint32_t log_n);
 int ecfft_run(ecg_ctx* ctx, int curve_id, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
               ecg_abort_cb abort_cb, void* user);
 int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const void* d_scalars,
-                  size_t line_len, size_t n_chunks, uint32_t window_bits, uint64_t* out_jac, hipStream_t s);
+                  int scalar_mont, size_t line_len, size_t n_chunks, uint32_t window_bits, uint64_t* out_jac,
+                  hipStream_t s);
 int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac);
 int gen_bases_run(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n,
                   void* d_out, hipStream_t s);

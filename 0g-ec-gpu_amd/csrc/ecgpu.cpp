@@ -190,6 +190,8 @@ int ecg_ctx_create(int device, ecg_ctx** out) {
   return ECG_OK;
 }
 
+static void base_cache_free(ecg_ctx* ctx);
+
 void ecg_ctx_destroy(ecg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
@@ -202,6 +204,7 @@ void ecg_ctx_destroy(ecg_ctx* ctx) {
       (void)hipEventDestroy(pr.second);
     }
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
+  base_cache_free(ctx);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -419,8 +422,8 @@ int ecg_msm_dev(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_s
 }
 
 int ecg_multiple_multiexp(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const uint64_t* scalars,
-                          int scalars_on_device, size_t line_len, size_t num_chunks, uint32_t window_bits,
-                          uint64_t* out_jac) {
+                          int scalars_on_device, int scalars_montgomery, size_t line_len, size_t num_chunks,
+                          uint32_t window_bits, uint64_t* out_jac) {
   ECG_TRY(ctx_enter(ctx));
   if (!out_jac || (n_bases && (!d_bases || !scalars))) {
     set_error("ecg_multiple_multiexp: null pointer");
@@ -434,7 +437,123 @@ int ecg_multiple_multiexp(ecg_ctx* ctx, int curve_id, const void* d_bases, size_
     ECG_HIP(hipMemcpyAsync(d, scalars, line_len * 32, hipMemcpyHostToDevice, s));
     d_sc = d;
   }
-  int rc = msm_batch_run(ctx, curve_id, d_bases, n_bases, d_sc, line_len, num_chunks, window_bits, out_jac, s);
+  int rc = msm_batch_run(ctx, curve_id, d_bases, n_bases, d_sc, scalars_montgomery, line_len, num_chunks,
+                         window_bits, out_jac, s);
+  (void)hipStreamSynchronize(s);
+  if (rc != ECG_OK) return rc;
+  return kt_collect(ctx);
+}
+
+static void base_cache_free(ecg_ctx* ctx) {
+  for (auto& e : ctx->base_cache)
+    if (e.dev) (void)hipFree(e.dev);
+  ctx->base_cache.clear();
+}
+
+void ecg_base_cache_clear(ecg_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  base_cache_free(ctx);
+}
+
+// Bases [x, y] on the device for (bases, layout, n): from the cache, or
+// uploaded (and converted from the ark layout) into `slot`.
+static int stage_bases(ecg_ctx* ctx, int curve_id, const void* bases, int layout, size_t n, int cache,
+                       const char* slot, void** d_xy) {
+  const size_t lq = fq_limbs64(curve_id);
+  const size_t xy_bytes = n * 2 * lq * 8;
+  const size_t raw_bytes = layout == ECG_BASES_ARK_AFFINE ? n * (2 * lq + 1) * 8 : xy_bytes;
+  hipStream_t s = ctx->stream;
+  if (cache) {
+    for (auto& e : ctx->base_cache)
+      if (e.host == bases && e.n == n && e.curve == curve_id && e.layout == layout) {
+        *d_xy = e.dev;
+        return ECG_OK;
+      }
+  }
+  void* dst;
+  if (cache) {
+    hipError_t e = hipMalloc(&dst, xy_bytes ? xy_bytes : 16);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("base cache: device allocation of %zu bytes failed: %s", xy_bytes, hipGetErrorString(e));
+      return ECG_ERR_NOMEM;
+    }
+  } else {
+    ECG_TRY(ws_get(ctx, slot, xy_bytes, &dst));
+  }
+  if (n) {
+    if (layout == ECG_BASES_ARK_AFFINE) {
+      void* raw;
+      ECG_TRY(ws_get(ctx, "prep_ark_raw", raw_bytes, &raw));
+      ECG_HIP(hipMemcpyAsync(raw, bases, raw_bytes, hipMemcpyHostToDevice, s));
+      ECG_TRY(bases_from_ark(ctx, curve_id, raw, n, dst, s));
+    } else {
+      ECG_HIP(hipMemcpyAsync(dst, bases, xy_bytes, hipMemcpyHostToDevice, s));
+    }
+  }
+  if (cache) {
+    if (ctx->base_cache.size() >= 8) {  // bounded: drop the oldest entry
+      ECG_HIP(hipStreamSynchronize(s));
+      (void)hipFree(ctx->base_cache.front().dev);
+      ctx->base_cache.erase(ctx->base_cache.begin());
+    }
+    ctx->base_cache.push_back({bases, n, curve_id, layout, dst});
+  }
+  *d_xy = dst;
+  return ECG_OK;
+}
+
+int ecg_msm_ex(ecg_ctx* ctx, int curve_id, const void* bases, int bases_layout, size_t n_bases, size_t skip,
+               const uint64_t* exps, int exps_montgomery, size_t n_exps, const uint64_t* density, int cache_bases,
+               uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
+  ECG_TRY(ctx_enter(ctx));
+  if (!out_jac || (n_exps && !exps) || (n_bases && !bases)) {
+    set_error("ecg_msm_ex: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  if (curve_id != ECG_CURVE_BLS12_381 && curve_id != ECG_CURVE_BN254) {
+    set_error("multiexp: unknown curve_id %d", curve_id);
+    return ECG_ERR_INVALID;
+  }
+  if (bases_layout != ECG_BASES_XY && bases_layout != ECG_BASES_ARK_AFFINE) {
+    set_error("ecg_msm_ex: unknown bases_layout %d", bases_layout);
+    return ECG_ERR_INVALID;
+  }
+  hipStream_t s = ctx->stream;
+  // exps -> device, density-compacted on device (generate_exps)
+  void *d_e, *d_ec;
+  ECG_TRY(ws_get(ctx, "msmx_exps", n_exps * 32, &d_e));
+  if (n_exps) ECG_HIP(hipMemcpyAsync(d_e, exps, n_exps * 32, hipMemcpyHostToDevice, s));
+  size_t dense = n_exps;
+  d_ec = d_e;
+  if (density) {
+    void* d_bits;
+    const size_t nw = (n_exps + 63) / 64;
+    ECG_TRY(ws_get(ctx, "msmx_bits", nw * 8, &d_bits));
+    if (nw) ECG_HIP(hipMemcpyAsync(d_bits, density, nw * 8, hipMemcpyHostToDevice, s));
+    ECG_TRY(ws_get(ctx, "msmx_exps_dense", n_exps * 32, &d_ec));
+    ECG_TRY(density_compact(ctx, d_e, (const uint64_t*)d_bits, n_exps, d_ec, &dense, s));
+  }
+  if (skip > n_bases || dense > n_bases - skip) {
+    set_error("Expected more bases from source.");  // multiexp_cpu.rs:55-61
+    return ECG_ERR_INVALID;
+  }
+  // bases: the whole (cached) array, or just the [skip, skip + dense) window
+  const size_t lq = fq_limbs64(curve_id);
+  void* d_xy;
+  const uint8_t* d_base0;
+  if (cache_bases) {
+    ECG_TRY(stage_bases(ctx, curve_id, bases, bases_layout, n_bases, 1, nullptr, &d_xy));
+    d_base0 = (const uint8_t*)d_xy + skip * 2 * lq * 8;
+  } else {
+    const size_t rec = bases_layout == ECG_BASES_ARK_AFFINE ? (2 * lq + 1) * 8 : 2 * lq * 8;
+    ECG_TRY(stage_bases(ctx, curve_id, (const uint8_t*)bases + skip * rec, bases_layout, dense, 0, "msmx_bases",
+                        &d_xy));
+    d_base0 = (const uint8_t*)d_xy;
+  }
+  int rc = msm_run(ctx, curve_id, d_base0, d_ec, dense, out_jac, s, abort_cb, user, exps_montgomery);
   (void)hipStreamSynchronize(s);
   if (rc != ECG_OK) return rc;
   return kt_collect(ctx);

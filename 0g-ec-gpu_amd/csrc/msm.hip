@@ -85,6 +85,7 @@ struct MsmGeom {
   uint32_t n_chunks;
   size_t line_len;
   size_t clen;
+  uint32_t scalar_mont;  // scalars arrive as Montgomery Fr elements (to_bigint on device)
   uint32_t tasks() const { return n_lines * n_chunks; }
 };
 
@@ -126,8 +127,16 @@ __global__ void __launch_bounds__(MSM_THREADS)
   if (j >= m) return;
   uint4 lo = scalars[2 * j], hi = scalars[2 * j + 1];
   uint32_t s[9] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, 0};
-  // reduce mod r (any 256-bit input; at most 2^256/r subtractions)
   using FrP = typename C::FrParams;
+  if (g.scalar_mont) {  // PrimeFieldRepr::to_bigint (ag-types/src/impls.rs:13) on device
+    Fp<FrP> m;
+#pragma unroll
+    for (int k = 0; k < 8; k++) m.v[k] = s[k];
+    m = from_mont(m);
+#pragma unroll
+    for (int k = 0; k < 8; k++) s[k] = m.v[k];
+  }
+  // reduce mod r (any 256-bit input; at most 2^256/r subtractions)
   for (int it = 0; it < 8; it++) {
     uint32_t t[8];
     int64_t c = 0;
@@ -504,7 +513,7 @@ static int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, 
 // window sums come back to the host, which runs the Horner fold.
 template <class C>
 static int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
-                        hipStream_t s, ecg_abort_cb abort_cb, void* user) {
+                        hipStream_t s, ecg_abort_cb abort_cb, void* user, uint32_t scalar_mont) {
   using F = typename C::Fq;
   using X = XYZZ<F>;
   using HP = typename C::FqParams;
@@ -516,7 +525,7 @@ static int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars
     if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144
     const size_t m = n - off < MSM_MAX_CHUNK ? n - off : MSM_MAX_CHUNK;
     const MsmPlan pl = make_plan(m, (uint32_t)C::FrParams::BITS);
-    const MsmGeom g{1, 1, m, m};
+    const MsmGeom g{1, 1, m, m, scalar_mont};
     void* d_sums;
     ECG_TRY(msm_core_t<C>(ctx, (const F*)d_bases + 2 * off, (const uint4*)d_scalars + 2 * off, g, pl, s, &d_sums));
     // window sums -> host; Horner fold over windows (multiexp.rs:221-233)
@@ -545,14 +554,16 @@ static int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars
 }
 
 int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
-            hipStream_t s, ecg_abort_cb abort_cb, void* user) {
+            hipStream_t s, ecg_abort_cb abort_cb, void* user, int scalar_mont) {
   if (n > 0x7fffffffull) {
     set_error("multiexp: at most 2^31-1 terms per call");
     return ECG_ERR_INVALID;
   }
   switch (curve_id) {
-    case ECG_CURVE_BLS12_381: return msm_single_t<BLS12_381>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user);
-    case ECG_CURVE_BN254: return msm_single_t<BN254>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user);
+    case ECG_CURVE_BLS12_381:
+      return msm_single_t<BLS12_381>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0);
+    case ECG_CURVE_BN254:
+      return msm_single_t<BN254>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0);
     default:
       set_error("multiexp: unknown curve_id %d", curve_id);
       return ECG_ERR_INVALID;
@@ -594,7 +605,8 @@ static int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars,
 }
 
 int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const void* d_scalars,
-                  size_t line_len, size_t n_chunks, uint32_t window_bits, uint64_t* out_jac, hipStream_t s) {
+                  int scalar_mont, size_t line_len, size_t n_chunks, uint32_t window_bits, uint64_t* out_jac,
+                  hipStream_t s) {
   if (line_len == 0 || n_chunks == 0) {
     set_error("multiple_multiexp: line_len and num_chunks must be positive");
     return ECG_ERR_INVALID;
@@ -617,7 +629,7 @@ int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_base
     set_error("multiple_multiexp: %zu tasks is too many", n_lines * n_chunks);
     return ECG_ERR_INVALID;
   }
-  const MsmGeom g{(uint32_t)n_lines, (uint32_t)n_chunks, line_len, line_len / n_chunks};
+  const MsmGeom g{(uint32_t)n_lines, (uint32_t)n_chunks, line_len, line_len / n_chunks, scalar_mont != 0};
   switch (curve_id) {
     case ECG_CURVE_BLS12_381: return msm_batch_t<BLS12_381>(ctx, d_bases, d_scalars, g, window_bits, out_jac, s);
     case ECG_CURVE_BN254: return msm_batch_t<BN254>(ctx, d_bases, d_scalars, g, window_bits, out_jac, s);

@@ -94,8 +94,12 @@ _SIGS = {
     "ecg_ec_fft_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, _u64p, ctypes.c_uint32,
                                       ctypes.c_void_p]),
     "ecg_multiple_multiexp": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
-                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
-                                             ctypes.c_uint32, _u64p]),
+                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                                             ctypes.c_size_t, ctypes.c_uint32, _u64p]),
+    "ecg_msm_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t,
+                                  ctypes.c_size_t, _u64p, ctypes.c_int, ctypes.c_size_t, _u64p, ctypes.c_int, _u64p,
+                                  ABORT_CB, ctypes.c_void_p]),
+    "ecg_base_cache_clear": (None, [ctypes.c_void_p]),
     "ecg_msm_check_bases": (ctypes.c_int, [ctypes.c_int, _u64p, _u64p, ctypes.c_size_t]),
     "ecg_gen_bases_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, ctypes.c_size_t,
                                          ctypes.c_void_p, ctypes.c_void_p]),
@@ -368,7 +372,7 @@ def upload_multiexp_bases(prog: Program, bases: np.ndarray) -> DeviceBuffer:
 
 def multiple_multiexp(prog: Program, bases_gpu: DeviceBuffer, exponents, num_chunks: int,
                       window_size: int = 0, neg_is_cheap: bool = True, curve="bls12_381",
-                      pin_window: bool = False) -> np.ndarray:
+                      pin_window: bool = False, exps_montgomery: bool = False) -> np.ndarray:
     """ag_cuda_ec::multiexp::multiple_multiexp (multiexp.rs:21-81).
 
     bases_gpu holds n_lines * len(exponents) bases; `exponents` is one row of
@@ -377,7 +381,9 @@ def multiple_multiexp(prog: Program, bases_gpu: DeviceBuffer, exponents, num_chu
     3*Lq) normalised Jacobian points, result[line * num_chunks + chunk].
     window_size / neg_is_cheap are the reference kernel's tuning knobs; results
     never depend on them.  The engine picks its own window unless
-    pin_window=True (then window_size in 1..22 is used as is)."""
+    pin_window=True (then window_size in 1..22 is used as is).
+    exps_montgomery=True takes Fr elements in Montgomery form and runs the
+    to_bigint conversion (benches/amt.rs:25-26, on the CPU there) on device."""
     cid = _curve(curve)
     lq = CURVE_FQ_LIMBS[cid]
     if isinstance(exponents, tuple):
@@ -395,7 +401,8 @@ def multiple_multiexp(prog: Program, bases_gpu: DeviceBuffer, exponents, num_chu
     out = np.zeros((n_lines * num_chunks, 3 * lq), dtype=np.uint64)
     wb = int(window_size) if pin_window else 0
     _check(lib().ecg_multiple_multiexp(prog.handle, cid, bases_gpu.ptr, n_lines * line_len, sc_ptr, on_dev,
-                                       line_len, num_chunks, wb, _ptr(out)), "multiple_multiexp")
+                                       int(exps_montgomery), line_len, num_chunks, wb, _ptr(out)),
+           "multiple_multiexp")
     del keep
     return out
 
@@ -606,6 +613,76 @@ def _curve(c) -> int:
     return cid
 
 
+class FullDensity:
+    """QueryDensity with every base present (multiexp_cpu.rs:96-115)."""
+
+    def generate_exps(self, exponents: np.ndarray) -> np.ndarray:
+        return exponents
+
+    def get_query_size(self):
+        return None
+
+
+class DensityTracker:
+    """bellman/ec-gpu DensityTracker (multiexp_cpu.rs:117-207): a bit per
+    exponent; set bits consume the (compacted) bases in order.  The product
+    path hands the packed bitmap to the device (`words()`); generate_exps here
+    is the host restatement used for inspection only."""
+
+    def __init__(self, bits=None):
+        self.bv = [] if bits is None else [bool(b) for b in bits]
+        self.total_density = sum(self.bv)
+
+    @staticmethod
+    def new() -> "DensityTracker":
+        return DensityTracker()
+
+    def add_element(self) -> None:
+        self.bv.append(False)
+
+    def inc(self, idx: int) -> None:
+        if not self.bv[idx]:
+            self.bv[idx] = True
+            self.total_density += 1
+
+    def get_total_density(self) -> int:
+        return self.total_density
+
+    def get_query_size(self) -> int:
+        return len(self.bv)
+
+    def extend(self, other: "DensityTracker", is_input_density: bool) -> None:
+        """multiexp_cpu.rs:162-206, including the coalesced first input."""
+        if not other.bv:
+            return
+        if not self.bv:
+            self.total_density = other.total_density
+            self.bv = list(other.bv)
+            return
+        if is_input_density:
+            if other.bv[0]:
+                if self.bv[0]:
+                    self.total_density -= 1
+                else:
+                    self.bv[0] = True
+            self.bv.extend(other.bv[1:])
+        else:
+            self.bv.extend(other.bv)
+        self.total_density += other.total_density
+
+    def words(self, n: int | None = None) -> np.ndarray:
+        """bitvec<usize, Lsb0> storage: bit i -> word i/64, bit i%64."""
+        n = len(self.bv) if n is None else n
+        bits = np.zeros(((n + 63) // 64) * 64, dtype=np.uint8)
+        m = min(n, len(self.bv))
+        bits[:m] = np.asarray(self.bv[:m], dtype=np.uint8)
+        return np.ascontiguousarray(np.packbits(bits, bitorder="little").view(np.uint64))
+
+    def generate_exps(self, exponents: np.ndarray) -> np.ndarray:
+        keep = np.asarray(self.bv[:len(exponents)], dtype=bool)
+        return exponents[:len(keep)][keep]
+
+
 class SingleMultiexpKernel:
     def __init__(self, prog: Program, cid: int, maybe_abort=None):
         self.program = prog
@@ -670,6 +747,35 @@ class MultiexpKernel:
         del keep
         _check(rc, "multiexp")
         return out
+
+    def multiexp_ex(self, bases: np.ndarray, exps: np.ndarray, skip: int = 0, density=None,
+                    exps_montgomery: bool = False, ark_affine: bool = False, cache_bases: bool = False) -> np.ndarray:
+        """multiexp with the reference's host prep moved on device (ecg_msm_ex,
+        first device): density-filtered exps (DensityTracker), Montgomery Fr
+        exps, arkworks Affine{x,y,infinity} bases ((n, 2*Lq+1) uint64 records),
+        and an optional persistent base cache."""
+        k = self.kernels[0]
+        cid = k.cid
+        lq = CURVE_FQ_LIMBS[cid]
+        rec = 2 * lq + 1 if ark_affine else 2 * lq
+        b = np.ascontiguousarray(bases, dtype=np.uint64).reshape(-1, rec)
+        e = np.ascontiguousarray(exps, dtype=np.uint64).reshape(-1, 4)
+        dens = None
+        if density is not None and not isinstance(density, FullDensity):
+            dens = density.words(e.shape[0])
+        out = np.zeros(3 * lq, dtype=np.uint64)
+        cb, keep = _abort_cb(k.maybe_abort)
+        with k.program._lock:
+            rc = lib().ecg_msm_ex(k.program.handle, cid, b.ctypes.data_as(ctypes.c_void_p), int(ark_affine),
+                                  b.shape[0], skip, _ptr(e), int(exps_montgomery), e.shape[0],
+                                  _ptr(dens) if dens is not None else None, int(cache_bases), _ptr(out), cb, None)
+        del keep
+        _check(rc, "multiexp")
+        return out
+
+    def clear_base_cache(self) -> None:
+        for k in self.kernels:
+            lib().ecg_base_cache_clear(k.program.handle)
 
 
 def check_bases(curve, bases: np.ndarray, exps: np.ndarray) -> None:

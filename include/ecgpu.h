@@ -151,8 +151,36 @@ int ecg_msm_dev(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_s
  * window_size; results never depend on it).  The reference's neg_is_cheap
  * flag has no analogue: digits are always signed. */
 int ecg_multiple_multiexp(ecg_ctx *ctx, int curve_id, const void *d_bases, size_t n_bases,
-                          const uint64_t *scalars, int scalars_on_device, size_t line_len,
-                          size_t num_chunks, uint32_t window_bits, uint64_t *out_jac);
+                          const uint64_t *scalars, int scalars_on_device, int scalars_montgomery,
+                          size_t line_len, size_t num_chunks, uint32_t window_bits,
+                          uint64_t *out_jac);
+
+/* ---- MSM with the reference's host-side prep done on device --
+ *   bases_layout ECG_BASES_XY          : [x, y] GpuRepr records (2 x Lq u64)
+ *                ECG_BASES_ARK_AFFINE  : arkworks Affine {x, y, infinity: bool}
+ *                                        records (2 x Lq u64 + 8 B), converted
+ *                                        on device (ag-types/src/impls.rs:48-58)
+ *   exps_montgomery != 0 : exps are Fr elements in Montgomery form; to_bigint
+ *                          (impls.rs:13) runs in the digit kernel
+ *   density != NULL      : bitmap of n_exps bits (bitvec Lsb0, u64 words); only
+ *                          exps with a set bit take part, consuming bases in
+ *                          order from `skip` -- DensityTracker::generate_exps
+ *                          (multiexp_cpu.rs:127-138) compacted on device, then
+ *                          MultiexpKernel::multiexp(bases, exps, skip)
+ *                          (multiexp.rs:372-400)
+ *   cache_bases != 0     : keep the converted bases resident, keyed by
+ *                          (bases pointer, n_bases, curve, layout); later calls
+ *                          with the same key skip the upload (the caller must
+ *                          not mutate the array; ecg_base_cache_clear drops it)
+ * Too few bases for the dense exps -> ECG_ERR_INVALID "Expected more bases
+ * from source." (multiexp_cpu.rs:55-61). */
+#define ECG_BASES_XY 0
+#define ECG_BASES_ARK_AFFINE 1
+int ecg_msm_ex(ecg_ctx *ctx, int curve_id, const void *bases, int bases_layout, size_t n_bases,
+               size_t skip, const uint64_t *exps, int exps_montgomery, size_t n_exps,
+               const uint64_t *density, int cache_bases, uint64_t *out_jac, ecg_abort_cb abort_cb,
+               void *user);
+void ecg_base_cache_clear(ecg_ctx *ctx);
 
 /* Sum `count` Jacobian points (3 x Lq u64 each, device memory) into one
  * normalised Jacobian point: the EC fold that follows the RCCL all-gather of
