@@ -70,6 +70,10 @@ struct ecg_ctx {
     void* dev = nullptr;
   };
   std::vector<BaseCache> base_cache;
+  // RCCL communicator of this rank (comm.cpp); size 1 / null = single GPU
+  void* comm = nullptr;
+  int comm_size = 1;
+  int comm_rank = 0;
   // kernel timing (HIP events on the launch stream)
   std::map<std::string, ecg::KernelTimes> ktimes;
   std::vector<hipEvent_t> event_pool;
@@ -113,6 +117,14 @@ int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count
 int ecfft_validate(int curve_id, uint32_t log_n);
 int ecfft_run(ecg_ctx* ctx, int curve_id, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
               ecg_abort_cb abort_cb, void* user);
+// distributed NTT (dfft.hip) and RCCL exchange (comm.cpp)
+int dfft_stage1(int field_id, const void* d_in, void* d_out, const uint64_t* omega, uint32_t T, uint32_t rank,
+                uint32_t log_n, hipStream_t s);
+int dfft_stage3(const void* d_in, void* d_out, uint32_t T, uint32_t log_n, hipStream_t s);
+int dfft_run(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omega, uint32_t log_n, hipStream_t s);
+int comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes_per_peer, hipStream_t s);
+void comm_free(ecg_ctx* ctx);
+int comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes, hipStream_t s);
 int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const void* d_scalars,
                   int scalar_mont, size_t line_len, size_t n_chunks, uint32_t window_bits, uint64_t* out_jac,
                   hipStream_t s);

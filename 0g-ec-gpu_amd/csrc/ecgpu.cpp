@@ -205,8 +205,16 @@ void ecg_ctx_destroy(ecg_ctx* ctx) {
     }
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
   base_cache_free(ctx);
+  comm_free(ctx);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+}
+
+int ecg_ctx_synchronize(ecg_ctx* ctx) {
+  ECG_TRY(ctx_enter(ctx));
+  ECG_HIP(hipStreamSynchronize(ctx->stream));
+  ECG_HIP(hipDeviceSynchronize());
+  return ECG_OK;
 }
 
 int ecg_ctx_info(ecg_ctx* ctx, size_t* mem_bytes, int* compute_units) {

@@ -100,6 +100,19 @@ _SIGS = {
                                   ctypes.c_size_t, _u64p, ctypes.c_int, ctypes.c_size_t, _u64p, ctypes.c_int, _u64p,
                                   ABORT_CB, ctypes.c_void_p]),
     "ecg_base_cache_clear": (None, [ctypes.c_void_p]),
+    "ecg_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "ecg_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "ecg_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
+    "ecg_comm_destroy": (None, [ctypes.c_void_p]),
+    "ecg_comm_allgather": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "ecg_comm_alltoall": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "ecg_msm_dist": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                    _u64p]),
+    "ecg_fft_dist": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, _u64p, ctypes.c_uint32]),
+    "ecg_fft_dist_stage1": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, _u64p,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    "ecg_fft_dist_stage3": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                           ctypes.c_uint32]),
     "ecg_msm_check_bases": (ctypes.c_int, [ctypes.c_int, _u64p, _u64p, ctypes.c_size_t]),
     "ecg_gen_bases_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, ctypes.c_size_t,
                                          ctypes.c_void_p, ctypes.c_void_p]),
@@ -271,6 +284,9 @@ class Program:
         cus = ctypes.c_int()
         _check(lib().ecg_ctx_info(self.handle, ctypes.byref(mem), ctypes.byref(cus)))
         return cus.value
+
+    def synchronize(self) -> None:
+        _check(lib().ecg_ctx_synchronize(self.handle), "synchronize")
 
     def kernel_time(self, name: str) -> tuple[float, int]:
         ms = ctypes.c_double()

@@ -10,12 +10,15 @@ Reference behaviour being replaced (ec-gpu-proxy):
 Here every rank owns one GPU.  MSM: each rank computes the partial sum of its
 range on its own GPU, the partials (one normalised Jacobian point, 144 B for
 BLS12-381) are all-gathered with RCCL over xGMI -- RCCL has no elliptic-curve
-reduction op -- and folded on the device (ecg_point_sum_dev).  FFT: whole
-transforms are assigned round-robin-by-chunk; nothing is exchanged.
+reduction op -- and folded (ecg_msm_dist).  FFT: whole transforms are
+assigned by chunk; nothing is exchanged.  One transform too large for a GPU,
+or already block-distributed, runs as ecg_fft_dist (three RCCL all-to-alls,
+dfft.hip).
 
-The compute and fold callables are injected so the same orchestration runs
-on the GPU (HIP kernels, backend "nccl") and in the CPU multi-process tests
-(backend "gloo").
+RCCL lives inside libecgpu (same HIP runtime as its device buffers);
+torch.distributed (any backend, gloo on CPU is enough) only carries the
+128-byte rendezvous id (comm_init).  msm_sharded keeps the orchestration
+injectable so the CPU multi-process tests (gloo) exercise the same split.
 """
 from __future__ import annotations
 
@@ -58,3 +61,96 @@ def msm_sharded(n: int, partial_fn: Callable[[int, int], "object"], fold_fn: Cal
     gathered = [torch.zeros_like(part) for _ in range(world)]
     dist.all_gather(gathered, part, group=group)
     return fold_fn(gathered)
+
+
+# ---------------------------------------------------------------------------
+# native RCCL path (libecgpu ecg_comm_* / ecg_msm_dist / ecg_fft_dist)
+# ---------------------------------------------------------------------------
+
+
+def comm_init(prog, rank: int, world: int, dist_mod=None, group=None) -> None:
+    """Rank 0 makes the RCCL id, the launcher's process group broadcasts it,
+    every rank binds its Program's context (ecg_comm_init)."""
+    import ctypes
+
+    import ecgpu
+
+    buf = (ctypes.c_uint8 * 128)()
+    if world > 1:
+        if dist_mod is None:
+            import torch.distributed as dist_mod
+        obj = [None]
+        if rank == 0:
+            ecgpu._check(ecgpu.lib().ecg_comm_unique_id(buf), "comm_unique_id")
+            obj = [bytes(buf)]
+        dist_mod.broadcast_object_list(obj, src=0, group=group)
+        ctypes.memmove(buf, obj[0], 128)
+    ecgpu._check(ecgpu.lib().ecg_comm_init(prog.handle, world, rank, buf), "comm_init")
+
+
+def msm_dist(prog, curve, d_bases, d_scalars, n_local: int):
+    """This rank's shard + RCCL all-gather of partials + fold -> full result."""
+    import numpy as np
+
+    import ecgpu
+
+    cid = ecgpu._curve(curve)
+    out = np.zeros(3 * ecgpu.CURVE_FQ_LIMBS[cid], dtype=np.uint64)
+    ecgpu._check(ecgpu.lib().ecg_msm_dist(prog.handle, cid, d_bases.ptr, d_scalars.ptr, n_local, ecgpu._ptr(out)),
+                 "msm_dist")
+    return out
+
+
+def fft_dist(prog, field, d_local, omega, log_n: int) -> None:
+    """One 2^log_n NTT, block-distributed over the communicator (in place)."""
+    import numpy as np
+
+    import ecgpu
+
+    om = np.ascontiguousarray(omega, dtype=np.uint64).reshape(4)
+    ecgpu._check(ecgpu.lib().ecg_fft_dist(prog.handle, ecgpu._fft_field(field), d_local.ptr, ecgpu._ptr(om), log_n),
+                 "fft_dist")
+
+
+def fft_dist_emulated(progs, field, d_blocks, omega, log_n: int) -> None:
+    """ecg_fft_dist's schedule for T block-buffers held in one process (one
+    context each, e.g. all on one GPU): the three all-to-alls are done by
+    host copies, the local steps by the same device kernels
+    (ecg_fft_dist_stage1/3, ecg_fft_dev).  Test and rehearsal harness for the
+    multi-rank path on a single-GPU box."""
+    import numpy as np
+
+    import ecgpu
+
+    T = len(d_blocks)
+    fid = ecgpu._fft_field(field)
+    lib = ecgpu.lib()
+    m = (1 << log_n) // T
+    seg = m // T
+    om = np.ascontiguousarray(omega, dtype=np.uint64).reshape(4)
+
+    def all_to_all(bufs):
+        host = [b.read(shape=(T, seg, 4)) for b in bufs]
+        for q in range(T):
+            bufs[q].write(np.ascontiguousarray(np.stack([host[s][q] for s in range(T)])))
+
+    tmp = [ecgpu.DeviceBuffer(p, m * 32) for p in progs]
+    all_to_all(d_blocks)
+    for r in range(T):
+        ecgpu._check(lib.ecg_fft_dist_stage1(progs[r].handle, fid, d_blocks[r].ptr, tmp[r].ptr, ecgpu._ptr(om),
+                                             T, r, log_n), "fft_dist_stage1")
+    all_to_all(tmp)
+    # local m-point NTT with omega^T
+    r_mod = {0: 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001,
+             2: 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001}[fid]
+    w = sum(int(om[i]) << (64 * i) for i in range(4)) * pow(1 << 256, -1, r_mod) % r_mod
+    wt = pow(w, T, r_mod) * (1 << 256) % r_mod
+    om_t = np.array([(wt >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+    for r in range(T):
+        ecgpu.fft_dev(progs[r], field, tmp[r], om_t, log_n - (T.bit_length() - 1))
+    all_to_all(tmp)
+    for r in range(T):
+        ecgpu._check(lib.ecg_fft_dist_stage3(progs[r].handle, tmp[r].ptr, d_blocks[r].ptr, T, log_n),
+                     "fft_dist_stage3")
+    for t in tmp:
+        t.free()

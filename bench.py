@@ -4,7 +4,9 @@
 Workload (BASELINE.json metric): one step = one G1 Pippenger MSM over 2^26
 (base, scalar) terms.  The terms are sharded in contiguous ranges across the N
 ranks (BASELINE config 4; at N=1 the whole 2^26 runs on one GPU).  The per-rank
-partial sums are all-gathered over RCCL (torch.distributed "nccl") and folded.
+partial sums are all-gathered over RCCL (linked into libecgpu, ecg_msm_dist)
+and folded; torch.distributed (gloo, CPU) only does the rendezvous, barriers
+and the max-over-ranks of the step time -- torch never touches the GPU.
 The NTT leg times one in-place 2^24 Fr NTT per rank per step (radix_fft_many
 semantics: whole transforms per GPU, no exchange); it is reported in "ntt".
 
@@ -39,6 +41,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 MAD_PEAK_T = 35.3              # measured v_mad_u64_u32 lane-ops/s, T/s (tools/mad_microbench.hip)
 R_BLS = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 R_BN = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
+P_BLS = int("1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab", 16)
+P_BN = 0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47
 MSM_SEED = 0x35A00026
 NTT_SEED = 0x0FF70024
 KAT_A = 0x1234567890ABCDEF1122334455667788
@@ -59,6 +63,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--msm-cpu-log", type=int, default=20)
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive API timings (N=1)")
+    ap.add_argument("--no-aux", action="store_true", help="skip the batched-MSM / EC-FFT side lines (N=1)")
     return ap.parse_args()
 
 
@@ -89,6 +95,27 @@ def rand_scalars(rng: np.random.Generator, n: int, r: int) -> np.ndarray:
     return out
 
 
+def pmc_traffic(kernel: str, streaming_read: bool):
+    """HBM bytes per launch (GB) from the committed rocprofv3 PMC passes
+    (tools/gpu_prof.sh -> profiles/<round>/pmc_fetch_write.json): FETCH_SIZE +
+    WRITE_SIZE.  gfx950 FETCH_SIZE counts half the bytes of wide coalesced
+    streaming reads (MI355X_MICROARCH.md, HBM/rocprofv3 section), so those are
+    doubled; gathers are reported as counted."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_fetch_write.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    for k, v in d.items():
+        if kernel in k:
+            fetch = v["FETCH_SIZE"]["mean_kb"] * 1024 / 1e9
+            write = v["WRITE_SIZE"]["mean_kb"] * 1024 / 1e9
+            return (2 * fetch if streaming_read else fetch) + write, os.path.relpath(files[-1], ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -96,21 +123,23 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = torch = None
     if world > 1:
-        # torch's HIP runtime must initialise before libecgpu's (two runtimes in
-        # one process); torch is only used for the RCCL collectives.
+        # Rendezvous only (CPU / gloo): the device exchange is RCCL inside
+        # libecgpu, on the same HIP runtime as its buffers.
         import torch
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        dev = torch.device("cuda", local_rank)
+        dist.init_process_group("gloo")
 
     cid = ecgpu.CURVE_NAMES[args.curve]
     fr_fid = ecgpu.CURVE_FR_FIELD[cid]
     lq = ecgpu.CURVE_FQ_LIMBS[cid]
     r_int = R_BLS if cid == 0 else R_BN
     prog = ecgpu.program(ecgpu.Device(local_rank))
+    if world > 1:
+        from ecgpu import dist as edist
+
+        edist.comm_init(prog, rank, world, dist)
 
     # ------------------------------------------------------------ MSM inputs (HBM-resident)
     n_total = 1 << args.msm_log
@@ -125,15 +154,11 @@ def main():
     result = np.zeros(3 * lq, dtype=np.uint64)
 
     def msm_step():
-        part = ecgpu.msm_dev(prog, args.curve, d_bases, d_scal, n_loc)
         if world == 1:
-            result[:] = part
+            result[:] = ecgpu.msm_dev(prog, args.curve, d_bases, d_scal, n_loc)
             return
-        t = torch.from_numpy(part.view(np.int64).copy()).to(dev)
-        g = torch.empty(world * t.numel(), dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(g, t)  # RCCL over xGMI: world x 144 B (no EC-add reduce op in RCCL)
-        parts = g.cpu().numpy().view(np.uint64)
-        ecgpu._check(ecgpu.lib().ecg_point_sum(cid, ecgpu._ptr(parts), world, ecgpu._ptr(result)), "fold")
+        # local MSM + RCCL all-gather of world x 144 B partials + fold (no EC-add reduce op in RCCL)
+        result[:] = edist.msm_dist(prog, args.curve, d_bases, d_scal, n_loc)
 
     # ------------------------------------------------------------ NTT inputs (HBM-resident)
     log_n = args.ntt_log
@@ -144,6 +169,12 @@ def main():
     for _ in range(log_n, two_adicity):
         omega = omega * omega % r_int
     omega_m = u64(omega * (1 << 256) % r_int)
+
+    def omega_for(ln: int) -> np.ndarray:
+        w = pow(gen, (r_int - 1) >> two_adicity, r_int)
+        for _ in range(ln, two_adicity):
+            w = w * w % r_int
+        return u64(w * (1 << 256) % r_int)
     ntt_in = rand_scalars(np.random.default_rng([NTT_SEED, rank]), n_ntt, r_int)  # any value < r is a Montgomery form
     d_ntt = ecgpu.DeviceBuffer.upload(prog, ntt_in)
 
@@ -152,14 +183,16 @@ def main():
         ecgpu.fft_dev(prog, args.curve + "_fr", d_ntt, omega_m, log_n)
 
     def barrier():
+        # every libecgpu call returns after its stream is synchronised, so the
+        # device is idle here; the barrier lines the ranks up
+        prog.synchronize()
         if world > 1:
             dist.barrier()
-            torch.cuda.synchronize()
 
     def max_over_ranks(x: float) -> float:
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -233,6 +266,62 @@ def main():
                     "sample": f"parallel_fft restatement at the full 2^{log_n}: {ntt_cpu_s:.2f} s wall"},
         }
 
+    # ------------------------------------------------------------ end-to-end API (PCIe-inclusive), N = 1
+    # The reference API takes host slices and copies them in and out on every
+    # call (multiexp.rs:163-164, fft.rs:89,129).  Not `value`: DESIGN.md §4.
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        host_bases = d_bases.read(shape=(n_loc, 2 * lq))
+        kern = ecgpu.MultiexpKernel.create([prog], [], args.curve)
+        pool = ecgpu.Worker()
+        kern.multiexp(pool, host_bases, scal, 0)
+        t_e = time.perf_counter()
+        out_e2e = kern.multiexp(pool, host_bases, scal, 0)
+        msm_e2e_s = time.perf_counter() - t_e
+        checks["msm_e2e_equals_resident"] = bool((out_e2e == result).all())
+        fk = ecgpu.FftKernel.create([prog], args.curve + "_fr")
+        host_ntt = ntt_in.copy()
+        fk.radix_fft(host_ntt, omega_m, log_n)
+        host_ntt = ntt_in.copy()
+        t_e = time.perf_counter()
+        fk.radix_fft(host_ntt, omega_m, log_n)
+        ntt_e2e_s = time.perf_counter() - t_e
+        e2e = {"msm_ms": msm_e2e_s * 1e3, "msm_terms_per_s": n_loc / msm_e2e_s,
+               "ntt_ms": ntt_e2e_s * 1e3, "ntt_elements_per_s": n_ntt / ntt_e2e_s,
+               "note": "host buffers in, host result out (H2D of 128 B/term, NTT H2D+D2H of 32 B/element)"}
+        del host_bases
+
+    # ------------------------------------------------------------ side lines (N = 1): SURVEY §8f rows
+    aux = None
+    if rank == 0 and world == 1 and not args.no_aux:
+        aux = {}
+        # batched multi-line MSM on the ag-cuda-ec AMT shape (benches/amt.rs: LOG_N=10 -> 2^21 x 10 lines)
+        L, lines, chunks = 1 << 21, 10, 1 << 10
+        d_lb = ecgpu.gen_bases_dev(prog, args.curve, 7, 11, L * lines)
+        d_le = ecgpu.DeviceBuffer.upload(prog, rand_scalars(np.random.default_rng(5), L, r_int))
+        ecgpu.multiple_multiexp(prog, d_lb, (d_le, L), chunks, curve=args.curve)
+        t_a = time.perf_counter()
+        ecgpu.multiple_multiexp(prog, d_lb, (d_le, L), chunks, curve=args.curve)
+        mm_s = time.perf_counter() - t_a
+        aux["multiple_multiexp"] = {"shape": f"{lines} lines x 2^21, {chunks} chunks/line ({L // chunks} terms/task)",
+                                    "ms": mm_s * 1e3, "terms_per_s": L * lines / mm_s}
+        d_lb.free()
+        d_le.free()
+        # G1 EC-FFT 2^16 (tests/ec_fft.rs top size)
+        le = 16
+        d_pts = ecgpu.gen_bases_dev(prog, args.curve, 3, 7, 1 << le)
+        aff = d_pts.read(shape=(1 << le, 2 * lq))
+        one = u64(((1 << (64 * lq)) % (P_BLS if cid == 0 else P_BN)), lq)
+        jac = np.ascontiguousarray(np.concatenate([aff, np.tile(one, (1 << le, 1))], axis=1))
+        d_jac = ecgpu.DeviceBuffer.upload(prog, jac)
+        om_e = omega_for(le)
+        ecgpu.ec_fft_dev(prog, args.curve, d_jac, om_e, le)
+        d_jac.write(jac)
+        t_a = time.perf_counter()
+        ecgpu.ec_fft_dev(prog, args.curve, d_jac, om_e, le)
+        ef_s = time.perf_counter() - t_a
+        aux["ec_fft"] = {"log_n": le, "ms": ef_s * 1e3, "butterflies_per_s": (1 << (le - 1)) * le / ef_s}
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -242,6 +331,8 @@ def main():
     # ------------------------------------------------------------ report
     bytes_per_term = 2 * lq * 8 + 32  # 96 B affine + 32 B scalar (BLS12-381), SURVEY §8(d)
     acc_achieved = bytes_per_term * n_loc / (acc_avg_ms / 1e3) / 1e9
+    acc_traffic, acc_src = pmc_traffic("msm_accumulate", streaming_read=False)
+    ntt_traffic, ntt_src = pmc_traffic("ntt_pass", streaming_read=True)
     ntt_achieved = 64 * n_ntt / (pass_avg_ms / 1e3) / 1e9
     # VALU evidence: v_mad_u64_u32 issued by the bucket accumulation (10 Fq muls
     # per XYZZ mixed add, one per term per window) vs the measured MAD roof.
@@ -264,17 +355,21 @@ def main():
                                f"+ Fr NTT 2^{log_n} per GPU", "msm_terms": n_total, "ntt_log_n": log_n,
                    "parallelism": f"range-shard x{world} + RCCL all-gather of partials" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "achieved": acc_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": acc_achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": acc_achieved / HBM_PEAK_GBS, "traffic": acc_traffic, "traffic_unit": "GB/launch",
+                     "traffic_source": acc_src,
                      "kernel": "msm_accumulate", "avg_ms": acc_avg_ms,
                      "note": "VALU int-MAD bound; achieved = 128 B/term x terms per launch / launch time"},
         "ntt": {"metric": f"Fr NTT elements/sec @2^{log_n}", "value": world * n_ntt / ntt_s,
                 "unit": "elements/s", "ms_per_ntt": ntt_s * 1e3, "scaling": "weak (one transform per GPU)",
                 "ms_kernels_per_ntt": pass_ms / args.steps, "passes": passes_per_ntt,
                 "roofline": {"bound": "hbm", "achieved": ntt_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": ntt_achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "ntt_pass",
+                             "frac": ntt_achieved / HBM_PEAK_GBS, "traffic": ntt_traffic,
+                             "traffic_unit": "GB/launch", "traffic_source": ntt_src, "kernel": "ntt_pass",
                              "avg_ms": pass_avg_ms}},
         "checks": checks,
         "cpu_baseline": cpu_baseline,
+        "e2e_api": e2e,
+        "aux": aux,
     }
     if W:
         mads = n_loc * W * 10 * MADS_FQ[cid]

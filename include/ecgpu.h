@@ -68,6 +68,8 @@ void ecg_ctx_destroy(ecg_ctx *ctx);
 /* device memory and compute units (Device::memory / compute_units,
  * used by multiexp.rs:109-127) */
 int ecg_ctx_info(ecg_ctx *ctx, size_t *mem_bytes, int *compute_units);
+/* Wait for all work on ctx's device (bench barriers). */
+int ecg_ctx_synchronize(ecg_ctx *ctx);
 const char *ecg_last_error(void);
 const char *ecg_version(void);
 
@@ -194,6 +196,34 @@ int ecg_point_sum(int curve_id, const uint64_t *points, size_t count, uint64_t *
  * CRS." if any base with a non-zero scalar is the identity -- the
  * reference CPU path's error behaviour (multiexp_cpu.rs:57-61). */
 int ecg_msm_check_bases(int curve_id, const uint64_t *bases_xy, const uint64_t *scalars, size_t n);
+
+/* ---- multi-GPU over RCCL (one process per GPU) ------------------
+ * Replace the reference's host-thread-per-device dispatch (multiexp.rs:324-367,
+ * fft.rs:211-246) for the one-process-per-GPU launch: rank 0 makes a 128-byte
+ * id, the launcher broadcasts it, every rank calls ecg_comm_init on its own
+ * context.  nranks = 1 needs no id (exchanges become device copies). */
+int ecg_comm_unique_id(uint8_t *out /* 128 bytes */);
+int ecg_comm_init(ecg_ctx *ctx, int nranks, int rank, const uint8_t *unique_id);
+void ecg_comm_destroy(ecg_ctx *ctx);
+/* RCCL all-gather / equal-split all-to-all of device buffers (synchronous). */
+int ecg_comm_allgather(ecg_ctx *ctx, const void *d_send, void *d_recv, size_t bytes);
+int ecg_comm_alltoall(ecg_ctx *ctx, const void *d_send, void *d_recv, size_t bytes_per_peer);
+/* MSM over this rank's contiguous shard (multiexp.rs:332-336 split); the
+ * partials are all-gathered over RCCL and folded (multiexp.rs:394-397), so
+ * every rank gets the full result in out_jac (host, 3 x Lq u64). */
+int ecg_msm_dist(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n_local,
+                 uint64_t *out_jac);
+/* One NTT of 2^log_n points, block-distributed (rank r holds points
+ * [r m, (r+1) m), m = 2^log_n / nranks), in place, natural order: the
+ * four-step split of parallel_fft (fft_cpu.rs:59-111) with three RCCL
+ * all-to-alls.  nranks a power of two <= 16, 2^log_n >= 2 nranks^2. */
+int ecg_fft_dist(ecg_ctx *ctx, int field_id, void *d_local, const uint64_t *omega, uint32_t log_n);
+/* Its local steps (for callers that drive the exchanges themselves):
+ * stage1: T-point DFT across the received segments + twiddle; stage3: the
+ * final [T][m/T] -> [m/T][T] interleave.  See dfft.hip for the layouts. */
+int ecg_fft_dist_stage1(ecg_ctx *ctx, int field_id, const void *d_in, void *d_out, const uint64_t *omega,
+                        uint32_t nranks, uint32_t rank, uint32_t log_n);
+int ecg_fft_dist_stage3(ecg_ctx *ctx, const void *d_in, void *d_out, uint32_t nranks, uint32_t log_n);
 
 /* ---- device buffers on ctx's device ---------------------------------------
  * Keep bases / polynomials resident in HBM across calls: the analogue of
