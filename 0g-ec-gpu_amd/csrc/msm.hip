@@ -13,22 +13,23 @@
 //  2. radix sort      (key, val) pairs, grouping each window's terms by bucket
 //                     (hipcub/rocPRIM onesweep).  Replaces the reference's
 //                     per-thread global-memory bucket RMW (multiexp_backup.cl:45-58).
-//  3. msm_bounds      bucket -> [start, end) in the sorted array.
-//  4. msm_accumulate  fixed-length segments of SEG sorted entries per thread
+//  3. msm_accumulate  fixed-length segments of SEG sorted entries per thread
 //                     (every lane runs exactly SEG XYZZ mixed adds, 8M+2S, of
 //                     gathered affine bases, negated for negative digits, with
 //                     a one-ahead gather prefetch): perfect lane balance
-//                     whatever the bucket-size distribution.  Runs wholly
-//                     inside a segment go straight to their bucket; runs that
-//                     cross a segment edge leave a partial in a 2-slot record.
+//                     whatever the bucket-size distribution.  Interior runs
+//                     are whole buckets and are stored; the first and last
+//                     run of each segment leave keyed partial records.
 //                     The dominant kernel: VALU-bound on v_mad_u64_u32.
-//  5. msm_fixup       one thread per bucket: empty -> identity, shared ->
-//                     sum of its segment partials.
-//  6. msm_reduce      per window, 2^(c-1)/LS segments of LS buckets: running
+//  4. msm_combine     the same fixed-segment scheme over the records, level
+//                     by level (32 records per thread, x16 fewer per level):
+//                     log-depth for any bucket skew.  Buckets without terms
+//                     keep the memset identity.
+//  5. msm_reduce      per window, 2^(c-1)/LS segments of LS buckets: running
 //                     sums (summation by parts, multiexp.cl:121-131) plus a
 //                     small-scalar multiple of the segment total.
-//  7. msm_sum         tree-fold of segment partials to one sum per window.
-//  8. host fold       Horner over windows (c doublings each) and the final
+//  6. msm_sum         tree-fold of segment partials to one sum per window.
+//  7. host fold       Horner over windows (c doublings each) and the final
 //                     affine normalisation on the host -- the reference GPU
 //                     path's own split (multiexp.rs:221-233): a serial chain of
 //                     ~256 doublings is ~25x faster on one CPU core than on one
@@ -48,6 +49,7 @@ namespace ecg {
 constexpr int MSM_THREADS = 256;
 constexpr uint32_t MSM_FOLD = 32;        // fan-in of the partial-sum tree
 constexpr size_t MSM_MAX_CHUNK = 1ull << 27;  // terms per device pass
+constexpr uint32_t MSM_COMBINE_SEG = 32;      // records per thread in msm_combine
 
 // Tunables (env overrides for A/B measurement in one build).
 static uint32_t env_u32(const char* name, uint32_t dflt) {
@@ -185,59 +187,46 @@ __global__ void __launch_bounds__(MSM_THREADS)
 }
 
 // ---------------------------------------------------------------------------
-// 3. bucket boundaries in the sorted key array
+// 3. bucket accumulation over fixed-length segments (dominant kernel)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(MSM_THREADS)
-    msm_bounds_kernel(const uint32_t* __restrict__ keys, size_t total, uint32_t sentinel,
-                      uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const uint32_t k = keys[i];
-  if (k >= sentinel) return;
-  if (i == 0 || keys[i - 1] != k) start[k] = (uint32_t)i;
-  if (i + 1 == total || keys[i + 1] != k) end[k] = (uint32_t)(i + 1);
-}
-
-// ---------------------------------------------------------------------------
-// 4. bucket accumulation over fixed-length segments (dominant kernel)
-// ---------------------------------------------------------------------------
-// Thread t owns sorted entries [t*SEG, (t+1)*SEG).  A run of bucket b is
-// "owned" when the whole bucket lies in one segment (start[b]/SEG ==
-// (end[b]-1)/SEG): its sum is final.  Otherwise the partial goes to record
-// slot 2t (b is the segment's first key) or 2t+1 (b is its last key).
-template <class C>
-ECG_DEV void acc_flush(uint32_t b, uint32_t first_key, const XYZZ<typename C::Fq>& acc, const uint32_t* start,
-                       const uint32_t* end, size_t t, uint32_t seg, XYZZ<typename C::Fq>* buckets,
-                       XYZZ<typename C::Fq>* recs) {
-  const uint32_t s0 = start[b], s1 = end[b];
-  if (s0 / seg == (s1 - 1) / seg) {
-    store_xyzz(&buckets[b], acc);
-  } else {
-    store_xyzz(&recs[2 * t + (b == first_key ? 0 : 1)], acc);
-  }
-}
+// Thread t owns sorted entries [t*SEG, (t+1)*SEG) and runs exactly SEG XYZZ
+// mixed adds, whatever the bucket-size distribution.  Runs strictly inside
+// the segment (another key on both sides) are whole buckets and are stored
+// directly.  The first and the last run -- which may continue in the
+// neighbouring segments -- are forwarded as keyed partial records
+// (rec[2t], rec[2t+1]); a single-run segment forwards its sum plus an
+// identity twin with the same key, so the record keys stay sorted with no
+// holes.  msm_combine_kernel sums the records level by level.
+constexpr uint32_t KEY_END = 0xffffffffu;
 
 template <class C>
 __global__ void __launch_bounds__(MSM_THREADS)
     msm_accumulate_kernel(const typename C::Fq* __restrict__ bases, const uint32_t* __restrict__ keys,
                           const uint32_t* __restrict__ vals, size_t total, uint32_t sentinel, uint32_t seg,
-                          const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
-                          XYZZ<typename C::Fq>* __restrict__ buckets, XYZZ<typename C::Fq>* __restrict__ recs) {
+                          XYZZ<typename C::Fq>* __restrict__ buckets, XYZZ<typename C::Fq>* __restrict__ recs,
+                          uint32_t* __restrict__ rkeys) {
   using F = typename C::Fq;
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t e0 = t * seg;
   if (e0 >= total) return;
   const size_t e1 = e0 + seg < total ? e0 + seg : total;
-  const uint32_t first_key = keys[e0];
-  if (first_key >= sentinel) return;
-  uint32_t b = first_key;
+  const XYZZ<F> zero = xyzz_zero<F>();
+  uint32_t b = keys[e0];
+  if (b >= sentinel) {  // all-zero-digit tail: no records
+    store_xyzz(&recs[2 * t], zero);
+    store_xyzz(&recs[2 * t + 1], zero);
+    rkeys[2 * t] = KEY_END;
+    rkeys[2 * t + 1] = KEY_END;
+    return;
+  }
   uint32_t v = vals[e0];
   Affine<F> P = load_affine(bases + 2 * (size_t)(v & 0x7fffffffu));
-  XYZZ<F> acc = xyzz_zero<F>();
+  XYZZ<F> acc = zero;
+  bool first_run = true;
   for (size_t e = e0; e < e1; e++) {
     // one-ahead prefetch of the next entry and its base
     const bool more = e + 1 < e1;
-    const uint32_t kn = more ? keys[e + 1] : sentinel;
+    const uint32_t kn = more ? keys[e + 1] : KEY_END;
     const uint32_t vn = more ? vals[e + 1] : 0u;
     Affine<F> Pn;
     if (kn < sentinel) Pn = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
@@ -247,41 +236,91 @@ __global__ void __launch_bounds__(MSM_THREADS)
       acc = xyzz_add_affine<F, true>(acc, P);
     }
     if (kn != b) {
-      acc_flush<C>(b, first_key, acc, start, end, t, seg, buckets, recs);
-      if (kn >= sentinel) return;
-      acc = xyzz_zero<F>();
+      const bool last = kn >= sentinel;  // end of segment or of the non-zero digits
+      if (first_run) {
+        store_xyzz(&recs[2 * t], acc);
+        rkeys[2 * t] = b;
+        if (last) {
+          store_xyzz(&recs[2 * t + 1], zero);
+          rkeys[2 * t + 1] = b;
+          return;
+        }
+        first_run = false;
+      } else if (last) {
+        store_xyzz(&recs[2 * t + 1], acc);
+        rkeys[2 * t + 1] = b;
+        return;
+      } else {
+        store_xyzz(&buckets[b], acc);  // interior run: a whole bucket
+      }
+      acc = zero;
       b = kn;
     }
     P = Pn;
     v = vn;
   }
-  acc_flush<C>(b, first_key, acc, start, end, t, seg, buckets, recs);
 }
 
 // ---------------------------------------------------------------------------
-// 5. bucket fix-up: empty -> identity; shared -> sum of segment partials
+// 4. record combine: the same fixed-segment scheme over keyed partials
+//    (full XYZZ adds).  Interior runs are whole buckets; first/last runs go
+//    to the next level (2 per segment), so each level shrinks the record
+//    count by seg/2 and the depth is logarithmic in the largest bucket --
+//    a bucket holding a large share of all terms (skewed scalars) costs
+//    O(log) levels, not a serial walk.  The last level (one segment) stores
+//    every run.  Buckets never written stay at the memset identity (ZZ = 0).
 // ---------------------------------------------------------------------------
 template <class C>
 __global__ void __launch_bounds__(MSM_THREADS)
-    msm_fixup_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ start,
-                     const uint32_t* __restrict__ end, uint32_t nbuckets, uint32_t seg,
-                     const XYZZ<typename C::Fq>* __restrict__ recs, XYZZ<typename C::Fq>* __restrict__ buckets) {
+    msm_combine_kernel(const XYZZ<typename C::Fq>* __restrict__ rin, const uint32_t* __restrict__ kin, size_t n,
+                       uint32_t sentinel, uint32_t seg, int final_level, XYZZ<typename C::Fq>* __restrict__ buckets,
+                       XYZZ<typename C::Fq>* __restrict__ rout, uint32_t* __restrict__ kout) {
   using F = typename C::Fq;
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbuckets) return;
-  const uint32_t s0 = start[b], s1 = end[b];
-  if (s1 == s0) {
-    store_xyzz(&buckets[b], xyzz_zero<F>());
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t e0 = t * seg;
+  if (e0 >= n) return;
+  const size_t e1 = e0 + seg < n ? e0 + seg : n;
+  const XYZZ<F> zero = xyzz_zero<F>();
+  uint32_t b = kin[e0];
+  if (b >= sentinel) {
+    if (!final_level) {
+      store_xyzz(&rout[2 * t], zero);
+      store_xyzz(&rout[2 * t + 1], zero);
+      kout[2 * t] = KEY_END;
+      kout[2 * t + 1] = KEY_END;
+    }
     return;
   }
-  const uint32_t t0 = s0 / seg, t1 = (s1 - 1) / seg;
-  if (t0 == t1) return;  // written by msm_accumulate
-  XYZZ<F> acc = xyzz_zero<F>();
-  for (uint32_t t = t0; t <= t1; t++) {
-    const uint32_t slot = keys[(size_t)t * seg] == b ? 0 : 1;
-    acc = xyzz_add<F, true>(acc, load_xyzz(&recs[2 * (size_t)t + slot]));
+  XYZZ<F> acc = zero;
+  bool first_run = true;
+  for (size_t e = e0; e < e1; e++) {
+    const uint32_t kn = e + 1 < e1 ? kin[e + 1] : KEY_END;
+    acc = xyzz_add<F, true>(acc, load_xyzz(&rin[e]));
+    if (kn != b) {
+      const bool last = kn >= sentinel;
+      if (final_level) {
+        store_xyzz(&buckets[b], acc);
+        if (last) return;
+      } else if (first_run) {
+        store_xyzz(&rout[2 * t], acc);
+        kout[2 * t] = b;
+        if (last) {
+          store_xyzz(&rout[2 * t + 1], zero);
+          kout[2 * t + 1] = b;
+          return;
+        }
+        first_run = false;
+      } else if (last) {
+        store_xyzz(&rout[2 * t + 1], acc);
+        kout[2 * t + 1] = b;
+        return;
+      } else {
+        store_xyzz(&buckets[b], acc);
+      }
+      acc = zero;
+      b = kn;
+    }
   }
-  store_xyzz(&buckets[b], acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -447,15 +486,17 @@ static int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, 
   while ((1ull << key_bits) <= sentinel) key_bits++;
   const size_t nseg = (total + pl.seg - 1) / pl.seg;
 
-  void *k0, *k1, *v0, *v1, *st, *en, *bk, *rc, *pa, *pb, *tmp;
+  void *k0, *k1, *v0, *v1, *bk, *rc, *rk, *rc2, *rk2, *pa, *pb, *tmp;
   ECG_TRY(ws_get(ctx, "msm_k0", total * 4, &k0));
   ECG_TRY(ws_get(ctx, "msm_k1", total * 4, &k1));
   ECG_TRY(ws_get(ctx, "msm_v0", total * 4, &v0));
   ECG_TRY(ws_get(ctx, "msm_v1", total * 4, &v1));
-  ECG_TRY(ws_get(ctx, "msm_start", (size_t)nb * 4, &st));
-  ECG_TRY(ws_get(ctx, "msm_end", (size_t)nb * 4, &en));
   ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nb * sizeof(X), &bk));
   ECG_TRY(ws_get(ctx, "msm_recs", 2 * nseg * sizeof(X), &rc));
+  ECG_TRY(ws_get(ctx, "msm_rkeys", 2 * nseg * 4, &rk));
+  const size_t nseg1 = (2 * nseg + MSM_COMBINE_SEG - 1) / MSM_COMBINE_SEG;
+  ECG_TRY(ws_get(ctx, "msm_recs2", 2 * nseg1 * sizeof(X), &rc2));
+  ECG_TRY(ws_get(ctx, "msm_rkeys2", 2 * nseg1 * 4, &rk2));
   ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
   ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * pl.S / MSM_FOLD + pl.G) * sizeof(X), &pb));
 
@@ -470,23 +511,34 @@ static int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, 
   ECG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
                                              (uint32_t*)v1, total, 0, key_bits, s));
 
-  ECG_HIP(hipMemsetAsync(st, 0, (size_t)nb * 4, s));
-  ECG_HIP(hipMemsetAsync(en, 0, (size_t)nb * 4, s));
-  hipLaunchKernelGGL(msm_bounds_kernel, dim3(blocks_for(total, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     (const uint32_t*)k1, total, sentinel, (uint32_t*)st, (uint32_t*)en);
-  ECG_HIP(hipGetLastError());
+  // buckets nobody writes (no term) stay the identity: all-zero XYZZ (ZZ = 0)
+  ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X), s));
 
   ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
   hipLaunchKernelGGL(msm_accumulate_kernel<C>, dim3(blocks_for(nseg, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     (const F*)d_bases, (const uint32_t*)k1, (const uint32_t*)v1, total, sentinel, pl.seg,
-                     (const uint32_t*)st, (const uint32_t*)en, (X*)bk, (X*)rc);
+                     (const F*)d_bases, (const uint32_t*)k1, (const uint32_t*)v1, total, sentinel, pl.seg, (X*)bk,
+                     (X*)rc, (uint32_t*)rk);
   ECG_HIP(hipGetLastError());
   ECG_TRY(kt_end(ctx, "msm_accumulate", s));
 
-  hipLaunchKernelGGL(msm_fixup_kernel<C>, dim3(blocks_for(nb, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     (const uint32_t*)k1, (const uint32_t*)st, (const uint32_t*)en, nb, pl.seg, (const X*)rc,
-                     (X*)bk);
-  ECG_HIP(hipGetLastError());
+  // combine the segment-edge partials, level by level
+  size_t nrec = 2 * nseg;
+  X* rin = (X*)rc;
+  uint32_t* kin = (uint32_t*)rk;
+  X* rout = (X*)rc2;
+  uint32_t* kout = (uint32_t*)rk2;
+  for (;;) {
+    const bool fin = nrec <= MSM_COMBINE_SEG;
+    const size_t nthr = (nrec + MSM_COMBINE_SEG - 1) / MSM_COMBINE_SEG;
+    hipLaunchKernelGGL(msm_combine_kernel<C>, dim3(blocks_for(nthr, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                       (const X*)rin, (const uint32_t*)kin, nrec, sentinel, MSM_COMBINE_SEG, fin ? 1 : 0, (X*)bk,
+                       rout, kout);
+    ECG_HIP(hipGetLastError());
+    if (fin) break;
+    nrec = 2 * nthr;
+    std::swap(rin, rout);
+    std::swap(kin, kout);
+  }
 
   hipLaunchKernelGGL(msm_reduce_kernel<C>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
                      dim3(MSM_THREADS), 0, s, (const X*)bk, pl, (X*)pa);
