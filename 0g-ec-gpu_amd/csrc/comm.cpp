@@ -122,13 +122,13 @@ int ecg_msm_dist(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_
     set_error("ecg_msm_dist: null pointer");
     return ECG_ERR_INVALID;
   }
-  if (curve_id != ECG_CURVE_BLS12_381 && curve_id != ECG_CURVE_BN254) {
+  if (!curve_valid(curve_id)) {
     set_error("multiexp: unknown curve_id %d", curve_id);
     return ECG_ERR_INVALID;
   }
   hipStream_t s = ctx->stream;
   const size_t pb = 3 * (size_t)fq_limbs64(curve_id) * 8;
-  uint64_t part[18];
+  uint64_t part[3 * ECG_MAX_COORD_U64];
   ECG_TRY(msm_run(ctx, curve_id, d_bases, d_scalars, n_local, part, s, nullptr, nullptr));
   void *d_part, *d_all;
   ECG_TRY(ws_get(ctx, "dist_part", pb, &d_part));

@@ -132,6 +132,17 @@ int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t*
 int gen_bases_run(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n,
                   void* d_out, hipStream_t s);
 
-inline int fq_limbs64(int curve_id) { return curve_id == ECG_CURVE_BLS12_381 ? 6 : 4; }
+// u64 words per point coordinate: Fq (G1) or Fq2 (G2); the largest is BLS12-381 G2.
+constexpr int ECG_MAX_COORD_U64 = 12;
+inline int fq_limbs64(int curve_id) {
+  switch (curve_id) {
+    case ECG_CURVE_BLS12_381: return 6;
+    case ECG_CURVE_BN254: return 4;
+    case ECG_CURVE_BLS12_381_G2: return 12;
+    case ECG_CURVE_BN254_G2: return 8;
+    default: return 0;
+  }
+}
+inline bool curve_valid(int curve_id) { return fq_limbs64(curve_id) != 0; }
 
 }  // namespace ecg

@@ -18,21 +18,42 @@
 // Identity: ZZ == 0 (XYZZ), Z == 0 (Jacobian, as ec.cl's POINT_ZERO=(0,1,0)),
 // and the all-zero affine pair (ag-types/src/impls.rs:52-54 GpuRepr).
 #pragma once
+#include <type_traits>
+
 #include "field.hpp"
+#include "field2.hpp"
 
 namespace ecg {
 
-template <class FqP, class FrP, class GenP>
+// A curve instance: coordinate field Fq (Fp for G1, Fp2 for G2), scalar field
+// Fr, generator constants.  EXT = degree of Fq over the base prime field.
+template <class FqP, class FrP, class GenP, int EXT_ = 1>
 struct CurveCfg {
-  using Fq = Fp<FqP>;
+  using Fq = std::conditional_t<EXT_ == 1, Fp<FqP>, Fp2<FqP>>;
   using Fr = Fp<FrP>;
   using FqParams = FqP;
   using FrParams = FrP;
   using Gen = GenP;
+  static constexpr int EXT = EXT_;
 };
 
 using BLS12_381 = CurveCfg<params::bls12_381_fq, params::bls12_381_fr, params::bls12_381_g1>;
 using BN254 = CurveCfg<params::bn254_fq, params::bn254_fr, params::bn254_g1>;
+// G2 over Fq2 (field2.hpp; ag-build/cl/field2.cl)
+using BLS12_381_G2 = CurveCfg<params::bls12_381_fq, params::bls12_381_fr, params::bls12_381_g2, 2>;
+using BN254_G2 = CurveCfg<params::bn254_fq, params::bn254_fr, params::bn254_g2, 2>;
+
+// Field element from little-endian u64 words (Montgomery), Fp or Fp2 (c0 first).
+template <class P>
+ECG_DEV void from_u64_words(Fp<P>& r, const uint64_t* w) {
+#pragma unroll
+  for (int i = 0; i < Fp<P>::L; i++) r.v[i] = (i & 1) ? (uint32_t)(w[i >> 1] >> 32) : (uint32_t)w[i >> 1];
+}
+template <class P>
+ECG_DEV void from_u64_words(Fp2<P>& r, const uint64_t* w) {
+  from_u64_words(r.c0, w);
+  from_u64_words(r.c1, w + P::N);
+}
 
 // Field-op policy
 template <class F, bool LZ>
@@ -41,7 +62,9 @@ struct Ops {
   static ECG_DEV F mul(const F& a, const F& b) {
     if constexpr (LZ) return fmul_lz(a, b); else return fmul(a, b);
   }
-  static ECG_DEV F sqr(const F& a) { return mul(a, a); }
+  static ECG_DEV F sqr(const F& a) {
+    if constexpr (LZ) return fsqr_lz(a); else return fsqr(a);
+  }
   static ECG_DEV F add(const F& a, const F& b) {
     if constexpr (LZ) return fadd_lz(a, b); else return fadd(a, b);
   }

@@ -22,6 +22,7 @@
 
 #include "ctx.hpp"
 #include "curve.hpp"
+#include "dispatch.hpp"
 
 namespace ecg {
 
@@ -131,14 +132,11 @@ static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t lo
 }
 
 int ecfft_validate(int curve_id, uint32_t log_n) {
-  uint32_t two_adicity;
-  switch (curve_id) {
-    case ECG_CURVE_BLS12_381: two_adicity = BLS12_381::FrParams::TWO_ADICITY; break;
-    case ECG_CURVE_BN254: two_adicity = BN254::FrParams::TWO_ADICITY; break;
-    default:
-      set_error("ec_fft: unknown curve_id %d", curve_id);
-      return ECG_ERR_INVALID;
-  }
+  uint32_t two_adicity = 0;
+  ECG_TRY(with_curve(curve_id, "ec_fft", [&](auto c) {
+    two_adicity = decltype(c)::FrParams::TWO_ADICITY;
+    return ECG_OK;
+  }));
   // ec_fft.rs:13 LOG2_MAX_ELEMENTS = 32; the Fr two-adicity bounds it further.
   if (log_n > two_adicity || log_n > 31) {
     set_error("ec_fft: log_n = %u exceeds the supported maximum (two-adicity %u, 2^31 points)", log_n, two_adicity);
@@ -150,10 +148,8 @@ int ecfft_validate(int curve_id, uint32_t log_n) {
 int ecfft_run(ecg_ctx* ctx, int curve_id, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
               ecg_abort_cb abort_cb, void* user) {
   ECG_TRY(ecfft_validate(curve_id, log_n));
-  switch (curve_id) {
-    case ECG_CURVE_BLS12_381: return ecfft_t<BLS12_381>(ctx, d_jac, omega, log_n, s, abort_cb, user);
-    default: return ecfft_t<BN254>(ctx, d_jac, omega, log_n, s, abort_cb, user);
-  }
+  return with_curve(curve_id, "ec_fft",
+                    [&](auto c) { return ecfft_t<decltype(c)>(ctx, d_jac, omega, log_n, s, abort_cb, user); });
 }
 
 }  // namespace ecg

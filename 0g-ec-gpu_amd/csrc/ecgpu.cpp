@@ -376,7 +376,7 @@ static int msm_host(ecg_ctx* ctx, int curve_id, const uint64_t* bases_xy, const 
     set_error("ecg_msm: null pointer");
     return ECG_ERR_INVALID;
   }
-  if (curve_id != ECG_CURVE_BLS12_381 && curve_id != ECG_CURVE_BN254) {
+  if (!curve_valid(curve_id)) {
     set_error("multiexp: unknown curve_id %d", curve_id);
     return ECG_ERR_INVALID;
   }
@@ -412,12 +412,12 @@ int ecg_msm_dev(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_s
     set_error("ecg_msm_dev: null pointer");
     return ECG_ERR_INVALID;
   }
-  if (curve_id != ECG_CURVE_BLS12_381 && curve_id != ECG_CURVE_BN254) {
+  if (!curve_valid(curve_id)) {
     set_error("multiexp: unknown curve_id %d", curve_id);
     return ECG_ERR_INVALID;
   }
   hipStream_t s = pick_stream(ctx, stream);
-  uint64_t host_out[18];
+  uint64_t host_out[3 * ECG_MAX_COORD_U64];
   const size_t ob = 3 * (size_t)fq_limbs64(curve_id) * 8;
   ECG_TRY(msm_run(ctx, curve_id, d_bases, d_scalars, n, host_out, s, nullptr, nullptr));
   if (out_on_device) {
@@ -521,7 +521,7 @@ int ecg_msm_ex(ecg_ctx* ctx, int curve_id, const void* bases, int bases_layout, 
     set_error("ecg_msm_ex: null pointer");
     return ECG_ERR_INVALID;
   }
-  if (curve_id != ECG_CURVE_BLS12_381 && curve_id != ECG_CURVE_BN254) {
+  if (!curve_valid(curve_id)) {
     set_error("multiexp: unknown curve_id %d", curve_id);
     return ECG_ERR_INVALID;
   }

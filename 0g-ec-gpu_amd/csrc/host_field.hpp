@@ -139,25 +139,64 @@ static inline HFp<P> hinv(const HFp<P>& a) {  // a^(p-2)
   return r;
 }
 
-// XYZZ points (x = X/ZZ, y = Y/ZZZ), identity ZZ == 0 -- same formulas as
-// the device code in curve.hpp (EFD g1p/auto-shortw-xyzz, a = 0).
+// Fq2 = Fq[u]/(u^2 + 1) on the host (G2 folds), c0 then c1 as on the device.
 template <class P>
-struct HXYZZ {
-  HFp<P> X, Y, ZZ, ZZZ;
-  bool is_zero() const { return ZZ.is_zero(); }
-  static HXYZZ zero() { return HXYZZ{HFp<P>::one(), HFp<P>::one(), HFp<P>::zero(), HFp<P>::zero()}; }
+struct HFp2 {
+  static constexpr int N = 2 * P::N;  // u64 words
+  HFp<P> c0, c1;
+  static HFp2 zero() { return HFp2{HFp<P>::zero(), HFp<P>::zero()}; }
+  static HFp2 one() { return HFp2{HFp<P>::one(), HFp<P>::zero()}; }
+  bool is_zero() const { return c0.is_zero() && c1.is_zero(); }
+  bool operator==(const HFp2& b) const { return c0 == b.c0 && c1 == b.c1; }
 };
 
 template <class P>
-static inline HXYZZ<P> hdbl(const HXYZZ<P>& p) {
+static inline HFp2<P> hadd(const HFp2<P>& a, const HFp2<P>& b) {
+  return HFp2<P>{hadd(a.c0, b.c0), hadd(a.c1, b.c1)};
+}
+template <class P>
+static inline HFp2<P> hsub(const HFp2<P>& a, const HFp2<P>& b) {
+  return HFp2<P>{hsub(a.c0, b.c0), hsub(a.c1, b.c1)};
+}
+template <class P>
+static inline HFp2<P> hmul(const HFp2<P>& a, const HFp2<P>& b) {
+  HFp<P> aa = hmul(a.c0, b.c0), bb = hmul(a.c1, b.c1);
+  HFp<P> t = hmul(hadd(a.c0, a.c1), hadd(b.c0, b.c1));
+  return HFp2<P>{hsub(aa, bb), hsub(hsub(t, aa), bb)};
+}
+template <class P>
+static inline HFp2<P> hinv(const HFp2<P>& a) {
+  HFp<P> t = hinv(hadd(hmul(a.c0, a.c0), hmul(a.c1, a.c1)));
+  HFp<P> z = HFp<P>::zero();
+  return HFp2<P>{hmul(a.c0, t), hsub(z, hmul(a.c1, t))};
+}
+template <class P>
+static inline HFp2<P> hcanon(HFp2<P> a) {
+  return HFp2<P>{hcanon(a.c0), hcanon(a.c1)};
+}
+
+// XYZZ points (x = X/ZZ, y = Y/ZZZ), identity ZZ == 0 -- same formulas as
+// the device code in curve.hpp (EFD g1p/auto-shortw-xyzz, a = 0), over any
+// coordinate field HF (HFp for G1, HFp2 for G2).
+template <class HF>
+struct HPoint {
+  HF X, Y, ZZ, ZZZ;
+  bool is_zero() const { return ZZ.is_zero(); }
+  static HPoint zero() { return HPoint{HF::one(), HF::one(), HF::zero(), HF::zero()}; }
+};
+template <class P>
+using HXYZZ = HPoint<HFp<P>>;
+
+template <class HF>
+static inline HPoint<HF> hdbl(const HPoint<HF>& p) {
   if (p.is_zero()) return p;
-  HFp<P> U = hadd(p.Y, p.Y);
-  HFp<P> V = hmul(U, U);
-  HFp<P> W = hmul(U, V);
-  HFp<P> S = hmul(p.X, V);
-  HFp<P> X2 = hmul(p.X, p.X);
-  HFp<P> M = hadd(hadd(X2, X2), X2);
-  HXYZZ<P> r;
+  HF U = hadd(p.Y, p.Y);
+  HF V = hmul(U, U);
+  HF W = hmul(U, V);
+  HF S = hmul(p.X, V);
+  HF X2 = hmul(p.X, p.X);
+  HF M = hadd(hadd(X2, X2), X2);
+  HPoint<HF> r;
   r.X = hsub(hsub(hmul(M, M), S), S);
   r.Y = hsub(hmul(M, hsub(S, r.X)), hmul(W, p.Y));
   r.ZZ = hmul(V, p.ZZ);
@@ -165,19 +204,19 @@ static inline HXYZZ<P> hdbl(const HXYZZ<P>& p) {
   return r;
 }
 
-template <class P>
-static inline HXYZZ<P> hadd_pts(const HXYZZ<P>& p, const HXYZZ<P>& q) {
+template <class HF>
+static inline HPoint<HF> hadd_pts(const HPoint<HF>& p, const HPoint<HF>& q) {
   if (p.is_zero()) return q;
   if (q.is_zero()) return p;
-  HFp<P> U1 = hmul(p.X, q.ZZ), U2 = hmul(q.X, p.ZZ);
-  HFp<P> S1 = hmul(p.Y, q.ZZZ), S2 = hmul(q.Y, p.ZZZ);
-  HFp<P> Pd = hsub(U2, U1), R = hsub(S2, S1);
+  HF U1 = hmul(p.X, q.ZZ), U2 = hmul(q.X, p.ZZ);
+  HF S1 = hmul(p.Y, q.ZZZ), S2 = hmul(q.Y, p.ZZZ);
+  HF Pd = hsub(U2, U1), R = hsub(S2, S1);
   if (Pd.is_zero()) {
     if (R.is_zero()) return hdbl(p);
-    return HXYZZ<P>::zero();
+    return HPoint<HF>::zero();
   }
-  HFp<P> PP = hmul(Pd, Pd), PPP = hmul(Pd, PP), Q = hmul(U1, PP);
-  HXYZZ<P> r;
+  HF PP = hmul(Pd, Pd), PPP = hmul(Pd, PP), Q = hmul(U1, PP);
+  HPoint<HF> r;
   r.X = hsub(hsub(hsub(hmul(R, R), PPP), Q), Q);
   r.Y = hsub(hmul(R, hsub(Q, r.X)), hmul(S1, PPP));
   r.ZZ = hmul(hmul(p.ZZ, q.ZZ), PP);
@@ -185,38 +224,43 @@ static inline HXYZZ<P> hadd_pts(const HXYZZ<P>& p, const HXYZZ<P>& q) {
   return r;
 }
 
-// Jacobian (X, Y, Z) -> XYZZ
-template <class P>
-static inline HXYZZ<P> hfrom_jac(const uint64_t* j) {
-  HXYZZ<P> r;
-  HFp<P> Z;
-  memcpy(r.X.v, j, sizeof r.X.v);
-  memcpy(r.Y.v, j + P::N, sizeof r.Y.v);
-  memcpy(Z.v, j + 2 * P::N, sizeof Z.v);
-  if (Z.is_zero()) return HXYZZ<P>::zero();
+// Jacobian (X, Y, Z), each coordinate HF::N u64 words -> XYZZ
+template <class HF>
+static inline HPoint<HF> hfrom_jac_t(const uint64_t* j) {
+  constexpr int N = HF::N;
+  HPoint<HF> r;
+  HF Z;
+  memcpy(&r.X, j, 8 * N);
+  memcpy(&r.Y, j + N, 8 * N);
+  memcpy(&Z, j + 2 * N, 8 * N);
+  if (Z.is_zero()) return HPoint<HF>::zero();
   r.ZZ = hmul(Z, Z);
   r.ZZZ = hmul(r.ZZ, Z);
   return r;
 }
+template <class P>
+static inline HXYZZ<P> hfrom_jac(const uint64_t* j) {
+  return hfrom_jac_t<HFp<P>>(j);
+}
 
 // normalised Jacobian (x, y, 1) or (0, 1, 0)
-template <class P>
-static inline void hto_jac_norm(const HXYZZ<P>& p, uint64_t* out) {
-  constexpr int N = P::N;
+template <class HF>
+static inline void hto_jac_norm(const HPoint<HF>& p, uint64_t* out) {
+  constexpr int N = HF::N;
   if (p.is_zero()) {
-    HFp<P> z = HFp<P>::zero(), o = HFp<P>::one();
-    memcpy(out, z.v, 8 * N);
-    memcpy(out + N, o.v, 8 * N);
-    memcpy(out + 2 * N, z.v, 8 * N);
+    HF z = HF::zero(), o = HF::one();
+    memcpy(out, &z, 8 * N);
+    memcpy(out + N, &o, 8 * N);
+    memcpy(out + 2 * N, &z, 8 * N);
     return;
   }
-  HFp<P> inv = hinv(hmul(p.ZZ, p.ZZZ));
-  HFp<P> x = hmul(p.X, hmul(inv, p.ZZZ));
-  HFp<P> y = hmul(p.Y, hmul(inv, p.ZZ));
-  HFp<P> o = HFp<P>::one();
-  memcpy(out, x.v, 8 * N);
-  memcpy(out + N, y.v, 8 * N);
-  memcpy(out + 2 * N, o.v, 8 * N);
+  HF inv = hinv(hmul(p.ZZ, p.ZZZ));
+  HF x = hmul(p.X, hmul(inv, p.ZZZ));
+  HF y = hmul(p.Y, hmul(inv, p.ZZ));
+  HF o = HF::one();
+  memcpy(out, &x, 8 * N);
+  memcpy(out + N, &y, 8 * N);
+  memcpy(out + 2 * N, &o, 8 * N);
 }
 
 }  // namespace host

@@ -1,608 +1,25 @@
-// Pippenger multi-scalar multiplication on G1 (BLS12-381, BN254) for gfx950.
-//
-// Replaces the reference's POINT_multiexp kernels (ag-build/cl/multiexp.cl:62-264,
-// multiexp_backup.cl:11-71) and SingleMultiexpKernel::multiexp's host driver
-// (ec-gpu-proxy/src/multiexp.rs:135-236).  Semantics follow multiexp_cpu
-// (multiexp_cpu.rs:244-367): out = sum_i s_i * P_i, compared in affine.
-//
-// Re-design:
-//  1. msm_digits      one thread per term: s mod r, signed c-bit windows
-//                     (digit in [-2^(c-1), 2^(c-1)], as multiexp.cl:95-119 but
-//                     applied to every window, carry-propagated), emits
-//                     (key = window*B + |d|-1, val = term | sign<<31).
-//  2. radix sort      (key, val) pairs, grouping each window's terms by bucket
-//                     (hipcub/rocPRIM onesweep).  Replaces the reference's
-//                     per-thread global-memory bucket RMW (multiexp_backup.cl:45-58).
-//  3. msm_accumulate  fixed-length segments of SEG sorted entries per thread
-//                     (every lane runs exactly SEG XYZZ mixed adds, 8M+2S, of
-//                     gathered affine bases, negated for negative digits, with
-//                     a one-ahead gather prefetch): perfect lane balance
-//                     whatever the bucket-size distribution.  Interior runs
-//                     are whole buckets and are stored; the first and last
-//                     run of each segment leave keyed partial records.
-//                     The dominant kernel: VALU-bound on v_mad_u64_u32.
-//  4. msm_combine     the same fixed-segment scheme over the records, level
-//                     by level (32 records per thread, x16 fewer per level):
-//                     log-depth for any bucket skew.  Buckets without terms
-//                     keep the memset identity.
-//  5. msm_reduce      per window, 2^(c-1)/LS segments of LS buckets: running
-//                     sums (summation by parts, multiexp.cl:121-131) plus a
-//                     small-scalar multiple of the segment total.
-//  6. msm_sum         tree-fold of segment partials to one sum per window.
-//  7. host fold       Horner over windows (c doublings each) and the final
-//                     affine normalisation on the host -- the reference GPU
-//                     path's own split (multiexp.rs:221-233): a serial chain of
-//                     ~256 doublings is ~25x faster on one CPU core than on one
-//                     GPU lane (host_field.hpp).
-#include <hipcub/hipcub.hpp>
-
-#include <cmath>
-#include <cstring>
+// curve_id dispatch of the MSM drivers.  The per-curve kernels and drivers
+// (msm_impl.hpp) are compiled once per curve in msm_inst.hip (-DECG_INST=id),
+// which exports one MsmOps table each; this file only routes calls.
 #include <vector>
 
 #include "ctx.hpp"
-#include "curve.hpp"
-#include "host_field.hpp"
+#include "msm_ops.hpp"
 
 namespace ecg {
 
-constexpr int MSM_THREADS = 256;
-constexpr uint32_t MSM_FOLD = 32;        // fan-in of the partial-sum tree
-constexpr size_t MSM_MAX_CHUNK = 1ull << 27;  // terms per device pass
-constexpr uint32_t MSM_COMBINE_SEG = 32;      // records per thread in msm_combine
+extern MsmOps msm_ops_0, msm_ops_1, msm_ops_2, msm_ops_3;
 
-// Tunables (env overrides for A/B measurement in one build).
-static uint32_t env_u32(const char* name, uint32_t dflt) {
-  const char* e = getenv(name);
-  return e ? (uint32_t)strtoul(e, nullptr, 10) : dflt;
-}
-static uint32_t msm_red_seg() {  // buckets per reduction segment
-  static uint32_t v = env_u32("ECG_MSM_RED_SEG", 64);
-  return v;
-}
-static uint32_t msm_acc_seg() {  // sorted entries per accumulation thread
-  static uint32_t v = env_u32("ECG_MSM_ACC_SEG", 128);
-  return v;
-}
-
-struct MsmPlan {
-  uint32_t c;     // window bits
-  uint32_t W;     // windows
-  uint32_t B;     // buckets per window = 2^(c-1)
-  uint32_t S;     // reduction segments per window
-  uint32_t LS;    // buckets per segment
-  uint32_t seg;   // sorted entries per accumulation thread
-  uint32_t G;     // bucket groups = tasks * W  (one group per (task, window))
-};
-
-// Task geometry.  A single MSM is one task (n_lines = n_chunks = 1).  The
-// batched form is ag-cuda-ec's multiple_multiexp (ag-cuda-ec/src/multiexp.rs:
-// 21-81, kernel ag-build/cl/multiexp.cl:215-262): n_lines lines of line_len
-// bases share one row of line_len scalars; each line is cut into n_chunks
-// chunks of clen = line_len / n_chunks terms (a remainder is ignored, as in
-// multiexp.cl:230), and task (line, chunk) computes
-//   sum_{i < clen} s[chunk*clen + i] * P[line*line_len + chunk*clen + i].
-struct MsmGeom {
-  uint32_t n_lines;
-  uint32_t n_chunks;
-  size_t line_len;
-  size_t clen;
-  uint32_t scalar_mont;  // scalars arrive as Montgomery Fr elements (to_bigint on device)
-  uint32_t tasks() const { return n_lines * n_chunks; }
-};
-
-// Window size minimising  n*W + W*B*4 + W*c*12  per task (bucket accumulation
-// vs reduction vs window-fold adds; a reduction step is ~2 full adds, ~1.4x a
-// mixed add).  nbits = scalar MODULUS_BIT_SIZE.  forced_c != 0 pins c.
-static MsmPlan make_plan(size_t n, uint32_t nbits, uint32_t forced_c = 0) {
-  double best = 1e300;
-  MsmPlan pl{};
-  for (uint32_t c = 1; c <= 22; c++) {
-    uint32_t W = (nbits + 1 + c - 1) / c;
-    double B = (double)(1u << (c - 1));
-    double cost = (double)n * W + W * B * 4.0 + W * c * 12.0;
-    if (forced_c ? c == forced_c : (c >= 2 && cost < best)) {
-      best = cost;
-      pl.c = c;
-      pl.W = W;
-    }
+static const MsmOps* msm_ops(int curve_id, const char* what) {
+  switch (curve_id) {
+    case ECG_CURVE_BLS12_381: return &msm_ops_0;
+    case ECG_CURVE_BN254: return &msm_ops_1;
+    case ECG_CURVE_BLS12_381_G2: return &msm_ops_2;
+    case ECG_CURVE_BN254_G2: return &msm_ops_3;
+    default:
+      set_error("%s: unknown curve_id %d", what, curve_id);
+      return nullptr;
   }
-  pl.B = 1u << (pl.c - 1);
-  pl.LS = pl.B < msm_red_seg() ? pl.B : msm_red_seg();
-  pl.S = pl.B / pl.LS;
-  pl.seg = msm_acc_seg();
-  pl.G = pl.W;
-  return pl;
-}
-
-// ---------------------------------------------------------------------------
-// 1. signed-digit decomposition
-// ---------------------------------------------------------------------------
-// One thread per scalar j of the row; the digits are emitted once per line
-// (entry (w, line, j) -> key = group(line, chunk(j), w) * B + |d| - 1).
-template <class C>
-__global__ void __launch_bounds__(MSM_THREADS)
-    msm_digits_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, uint32_t* __restrict__ keys,
-                      uint32_t* __restrict__ vals) {
-  const size_t m = (size_t)g.n_chunks * g.clen;
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
-  uint4 lo = scalars[2 * j], hi = scalars[2 * j + 1];
-  uint32_t s[9] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, 0};
-  using FrP = typename C::FrParams;
-  if (g.scalar_mont) {  // PrimeFieldRepr::to_bigint (ag-types/src/impls.rs:13) on device
-    Fp<FrP> m;
-#pragma unroll
-    for (int k = 0; k < 8; k++) m.v[k] = s[k];
-    m = from_mont(m);
-#pragma unroll
-    for (int k = 0; k < 8; k++) s[k] = m.v[k];
-  }
-  // reduce mod r (any 256-bit input; at most 2^256/r subtractions)
-  for (int it = 0; it < 8; it++) {
-    uint32_t t[8];
-    int64_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      c = (int64_t)s[k] - Fp<FrP>::p32(k) + (c >> 32);
-      t[k] = (uint32_t)c;
-    }
-    if ((c >> 32) & 1) break;  // s < r
-#pragma unroll
-    for (int k = 0; k < 8; k++) s[k] = t[k];
-  }
-  const uint32_t chunk = g.n_chunks == 1 ? 0u : (uint32_t)(j / g.clen);
-  const uint32_t mask = (1u << pl.c) - 1;
-  const uint32_t half = 1u << (pl.c - 1);
-  const uint32_t sentinel = pl.G * pl.B;
-  uint32_t carry = 0;
-  for (uint32_t w = 0; w < pl.W; w++) {
-    const uint32_t bit = w * pl.c;
-    const uint32_t limb = bit >> 5, sh = bit & 31;
-    uint32_t v = 0;
-    if (limb < 8) {
-      uint64_t two = (uint64_t)s[limb] | ((uint64_t)s[limb + 1] << 32);
-      v = (uint32_t)(two >> sh) & mask;
-    }
-    int32_t d = (int32_t)(v + carry);
-    carry = 0;
-    if (w + 1 < pl.W && (uint32_t)d >= half) {
-      d -= (int32_t)(1u << pl.c);
-      carry = 1;
-    }
-    const uint32_t mag = d < 0 ? (uint32_t)(-d) : (uint32_t)d;
-    const uint32_t sign = d < 0 ? 0x80000000u : 0u;
-    for (uint32_t l = 0; l < g.n_lines; l++) {
-      const size_t o = ((size_t)w * g.n_lines + l) * m + j;
-      if (d == 0) {
-        keys[o] = sentinel;
-        vals[o] = 0;
-      } else {
-        const uint32_t grp = (l * g.n_chunks + chunk) * pl.W + w;
-        keys[o] = grp * pl.B + (mag - 1);
-        vals[o] = (uint32_t)(l * g.line_len + j) | sign;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// 3. bucket accumulation over fixed-length segments (dominant kernel)
-// ---------------------------------------------------------------------------
-// Thread t owns sorted entries [t*SEG, (t+1)*SEG) and runs exactly SEG XYZZ
-// mixed adds, whatever the bucket-size distribution.  Runs strictly inside
-// the segment (another key on both sides) are whole buckets and are stored
-// directly.  The first and the last run -- which may continue in the
-// neighbouring segments -- are forwarded as keyed partial records
-// (rec[2t], rec[2t+1]); a single-run segment forwards its sum plus an
-// identity twin with the same key, so the record keys stay sorted with no
-// holes.  msm_combine_kernel sums the records level by level.
-constexpr uint32_t KEY_END = 0xffffffffu;
-
-template <class C>
-__global__ void __launch_bounds__(MSM_THREADS)
-    msm_accumulate_kernel(const typename C::Fq* __restrict__ bases, const uint32_t* __restrict__ keys,
-                          const uint32_t* __restrict__ vals, size_t total, uint32_t sentinel, uint32_t seg,
-                          XYZZ<typename C::Fq>* __restrict__ buckets, XYZZ<typename C::Fq>* __restrict__ recs,
-                          uint32_t* __restrict__ rkeys) {
-  using F = typename C::Fq;
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t e0 = t * seg;
-  if (e0 >= total) return;
-  const size_t e1 = e0 + seg < total ? e0 + seg : total;
-  const XYZZ<F> zero = xyzz_zero<F>();
-  uint32_t b = keys[e0];
-  if (b >= sentinel) {  // all-zero-digit tail: no records
-    store_xyzz(&recs[2 * t], zero);
-    store_xyzz(&recs[2 * t + 1], zero);
-    rkeys[2 * t] = KEY_END;
-    rkeys[2 * t + 1] = KEY_END;
-    return;
-  }
-  uint32_t v = vals[e0];
-  Affine<F> P = load_affine(bases + 2 * (size_t)(v & 0x7fffffffu));
-  XYZZ<F> acc = zero;
-  bool first_run = true;
-  for (size_t e = e0; e < e1; e++) {
-    // one-ahead prefetch of the next entry and its base
-    const bool more = e + 1 < e1;
-    const uint32_t kn = more ? keys[e + 1] : KEY_END;
-    const uint32_t vn = more ? vals[e + 1] : 0u;
-    Affine<F> Pn;
-    if (kn < sentinel) Pn = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
-    if (!aff_is_identity(P)) {  // GpuRepr identity (impls.rs:52-54) contributes nothing
-      F ny = fneg_lz(P.y);  // 2p - y: one subtraction (lazy range)
-      if (v >> 31) P.y = ny;
-      acc = xyzz_add_affine<F, true>(acc, P);
-    }
-    if (kn != b) {
-      const bool last = kn >= sentinel;  // end of segment or of the non-zero digits
-      if (first_run) {
-        store_xyzz(&recs[2 * t], acc);
-        rkeys[2 * t] = b;
-        if (last) {
-          store_xyzz(&recs[2 * t + 1], zero);
-          rkeys[2 * t + 1] = b;
-          return;
-        }
-        first_run = false;
-      } else if (last) {
-        store_xyzz(&recs[2 * t + 1], acc);
-        rkeys[2 * t + 1] = b;
-        return;
-      } else {
-        store_xyzz(&buckets[b], acc);  // interior run: a whole bucket
-      }
-      acc = zero;
-      b = kn;
-    }
-    P = Pn;
-    v = vn;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// 4. record combine: the same fixed-segment scheme over keyed partials
-//    (full XYZZ adds).  Interior runs are whole buckets; first/last runs go
-//    to the next level (2 per segment), so each level shrinks the record
-//    count by seg/2 and the depth is logarithmic in the largest bucket --
-//    a bucket holding a large share of all terms (skewed scalars) costs
-//    O(log) levels, not a serial walk.  The last level (one segment) stores
-//    every run.  Buckets never written stay at the memset identity (ZZ = 0).
-// ---------------------------------------------------------------------------
-template <class C>
-__global__ void __launch_bounds__(MSM_THREADS)
-    msm_combine_kernel(const XYZZ<typename C::Fq>* __restrict__ rin, const uint32_t* __restrict__ kin, size_t n,
-                       uint32_t sentinel, uint32_t seg, int final_level, XYZZ<typename C::Fq>* __restrict__ buckets,
-                       XYZZ<typename C::Fq>* __restrict__ rout, uint32_t* __restrict__ kout) {
-  using F = typename C::Fq;
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t e0 = t * seg;
-  if (e0 >= n) return;
-  const size_t e1 = e0 + seg < n ? e0 + seg : n;
-  const XYZZ<F> zero = xyzz_zero<F>();
-  uint32_t b = kin[e0];
-  if (b >= sentinel) {
-    if (!final_level) {
-      store_xyzz(&rout[2 * t], zero);
-      store_xyzz(&rout[2 * t + 1], zero);
-      kout[2 * t] = KEY_END;
-      kout[2 * t + 1] = KEY_END;
-    }
-    return;
-  }
-  XYZZ<F> acc = zero;
-  bool first_run = true;
-  for (size_t e = e0; e < e1; e++) {
-    const uint32_t kn = e + 1 < e1 ? kin[e + 1] : KEY_END;
-    acc = xyzz_add<F, true>(acc, load_xyzz(&rin[e]));
-    if (kn != b) {
-      const bool last = kn >= sentinel;
-      if (final_level) {
-        store_xyzz(&buckets[b], acc);
-        if (last) return;
-      } else if (first_run) {
-        store_xyzz(&rout[2 * t], acc);
-        kout[2 * t] = b;
-        if (last) {
-          store_xyzz(&rout[2 * t + 1], zero);
-          kout[2 * t + 1] = b;
-          return;
-        }
-        first_run = false;
-      } else if (last) {
-        store_xyzz(&rout[2 * t + 1], acc);
-        kout[2 * t + 1] = b;
-        return;
-      } else {
-        store_xyzz(&buckets[b], acc);
-      }
-      acc = zero;
-      b = kn;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// 5. per-segment summation by parts
-// ---------------------------------------------------------------------------
-template <class C>
-__global__ void __launch_bounds__(MSM_THREADS)
-    msm_reduce_kernel(const XYZZ<typename C::Fq>* __restrict__ buckets, MsmPlan pl,
-                      XYZZ<typename C::Fq>* __restrict__ partial) {
-  using F = typename C::Fq;
-  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= pl.G * pl.S) return;
-  const uint32_t w = id / pl.S, sgm = id % pl.S;
-  const XYZZ<F>* bk = buckets + (size_t)w * pl.B + (size_t)sgm * pl.LS;
-  XYZZ<F> run = xyzz_zero<F>(), acc = xyzz_zero<F>();
-  for (int j = (int)pl.LS - 1; j >= 0; j--) {
-    run = xyzz_add<F, true>(run, load_xyzz(&bk[j]));
-    acc = xyzz_add<F, true>(acc, run);
-  }
-  // acc = sum_j (j+1) S_j ; add (sgm*LS) * run for the segment offset
-  if (sgm != 0) acc = xyzz_add<F, true>(acc, xyzz_mul_small<F, true>(run, sgm * pl.LS));
-  store_xyzz(&partial[id], acc);
-}
-
-// ---------------------------------------------------------------------------
-// 6. fold `cnt` consecutive points per group into ceil(cnt / MSM_FOLD)
-// ---------------------------------------------------------------------------
-template <class C>
-__global__ void __launch_bounds__(MSM_THREADS)
-    msm_sum_kernel(const XYZZ<typename C::Fq>* __restrict__ in, uint32_t W, uint32_t cnt, uint32_t out_cnt,
-                   XYZZ<typename C::Fq>* __restrict__ out) {
-  using F = typename C::Fq;
-  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= W * out_cnt) return;
-  const uint32_t w = id / out_cnt, o = id % out_cnt;
-  const uint32_t j0 = o * MSM_FOLD, j1 = min(j0 + MSM_FOLD, cnt);
-  XYZZ<F> acc = xyzz_zero<F>();
-  for (uint32_t j = j0; j < j1; j++) acc = xyzz_add<F, true>(acc, load_xyzz(&in[(size_t)w * cnt + j]));
-  store_xyzz(&out[id], acc);
-}
-
-// ---------------------------------------------------------------------------
-// Synthetic bases P_i = (a + i*b) G  (bench/test input generator)
-// ---------------------------------------------------------------------------
-constexpr uint32_t GEN_BLOCK = 64;  // points per thread (batch-normalised)
-
-template <class C>
-ECG_DEV XYZZ<typename C::Fq> gen_mul(const uint32_t* k) {  // k (8 x u32 canonical) * G
-  using F = typename C::Fq;
-  Affine<F> g;
-#pragma unroll
-  for (int i = 0; i < F::L; i++) {
-    g.x.v[i] = (i & 1) ? (uint32_t)(C::Gen::GX[i >> 1] >> 32) : (uint32_t)C::Gen::GX[i >> 1];
-    g.y.v[i] = (i & 1) ? (uint32_t)(C::Gen::GY[i >> 1] >> 32) : (uint32_t)C::Gen::GY[i >> 1];
-  }
-  XYZZ<F> acc = xyzz_zero<F>();
-  for (int bit = 255; bit >= 0; bit--) {
-    acc = xyzz_dbl(acc);
-    if ((k[bit >> 5] >> (bit & 31)) & 1) acc = xyzz_add_affine(acc, g);
-  }
-  return acc;
-}
-
-template <class C>
-__global__ void gen_step_kernel(Fp<typename C::FrParams> bc, typename C::Fq* __restrict__ q_aff) {
-  using F = typename C::Fq;
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  Affine<F> a = xyzz_to_affine(gen_mul<C>(bc.v));
-  store(&q_aff[0], a.x);
-  store(&q_aff[1], a.y);
-}
-
-template <class C>
-__global__ void __launch_bounds__(MSM_THREADS)
-    gen_bases_kernel(Fp<typename C::FrParams> ac, Fp<typename C::FrParams> bc, size_t n,
-                     const typename C::Fq* __restrict__ q_aff, typename C::Fq* __restrict__ out,
-                     typename C::Fq* __restrict__ scratch) {
-  using F = typename C::Fq;
-  using S = Fp<typename C::FrParams>;
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t i0 = t * GEN_BLOCK;
-  if (i0 >= n) return;
-  const uint32_t cnt = (uint32_t)min((size_t)GEN_BLOCK, n - i0);
-  // s0 = a + i0*b (mod r)
-  const S am = to_mont(ac), bm = to_mont(bc);
-  S im = S::zero();
-  im.v[0] = (uint32_t)i0;
-  im.v[1] = (uint32_t)(i0 >> 32);
-  im = to_mont(im);
-  S s0 = from_mont(fadd(am, fmul(bm, im)));
-  XYZZ<F> P = gen_mul<C>(s0.v);
-  Affine<F> Q = load_affine(q_aff);
-  // walk and stash X, Y in out, ZZ, ZZZ and prefix products in scratch
-  F pref = F::one();
-  for (uint32_t k = 0; k < cnt; k++) {
-    const size_t i = i0 + k;
-    store(&out[2 * i], P.X);
-    store(&out[2 * i + 1], P.Y);
-    store(&scratch[3 * i], P.ZZ);
-    store(&scratch[3 * i + 1], P.ZZZ);
-    store(&scratch[3 * i + 2], pref);
-    pref = fmul(pref, fmul(P.ZZ, P.ZZZ));
-    P = xyzz_add_affine(P, Q);
-  }
-  F inv = finv(pref);
-  for (int k = (int)cnt - 1; k >= 0; k--) {
-    const size_t i = i0 + k;
-    F zz = load(&scratch[3 * i]), zzz = load(&scratch[3 * i + 1]), pr = load(&scratch[3 * i + 2]);
-    F d_inv = fmul(inv, pr);  // 1 / (ZZ*ZZZ) of point i
-    inv = fmul(inv, fmul(zz, zzz));
-    F x = fmul(load(&out[2 * i]), fmul(d_inv, zzz));
-    F y = fmul(load(&out[2 * i + 1]), fmul(d_inv, zz));
-    store(&out[2 * i], x);
-    store(&out[2 * i + 1], y);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// 7. batched form: per-task Horner fold over its W window sums + affine
-//    normalisation, one thread per task (the single-MSM path folds on the
-//    host instead, see msm_single_t).  Output: normalised Jacobian (x, y, 1)
-//    or (0, 1, 0), the reference's G::Curve layout (multiexp.cl:259-261
-//    writes one Jacobian per task).
-// ---------------------------------------------------------------------------
-template <class C>
-__global__ void __launch_bounds__(64)
-    msm_fold_kernel(const XYZZ<typename C::Fq>* __restrict__ sums, MsmPlan pl, uint32_t tasks,
-                    typename C::Fq* __restrict__ out) {
-  using F = typename C::Fq;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= tasks) return;
-  XYZZ<F> acc = xyzz_zero<F>();
-  for (int w = (int)pl.W - 1; w >= 0; w--) {
-    if (w != (int)pl.W - 1)
-      for (uint32_t k = 0; k < pl.c; k++) acc = xyzz_dbl<F, true>(acc);
-    acc = xyzz_add<F, true>(acc, load_xyzz(&sums[(size_t)t * pl.W + w]));
-  }
-  acc = xyzz_canon(acc);
-  const bool id = xyzz_is_zero(acc);
-  Jac<F> j = jac_from_affine_norm(xyzz_to_affine(acc), id);
-  store(&out[3 * (size_t)t], j.X);
-  store(&out[3 * (size_t)t + 1], j.Y);
-  store(&out[3 * (size_t)t + 2], j.Z);
-}
-
-// ---------------------------------------------------------------------------
-// host drivers
-// ---------------------------------------------------------------------------
-static inline uint32_t blocks_for(size_t n, int threads) { return (uint32_t)((n + threads - 1) / threads); }
-
-// Steps 1-6 for one device pass: leaves pl.G window sums (lazy XYZZ) on the
-// device and returns their address in *d_sums.
-template <class C>
-static int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
-                      const MsmPlan& pl, hipStream_t s, void** d_sums) {
-  using F = typename C::Fq;
-  using X = XYZZ<F>;
-  const size_t m = (size_t)g.n_chunks * g.clen;  // scalars consumed
-  const size_t total = (size_t)pl.W * g.n_lines * m;
-  const uint32_t nb = pl.G * pl.B;
-  const uint32_t sentinel = nb;
-  int key_bits = 1;
-  while ((1ull << key_bits) <= sentinel) key_bits++;
-  const size_t nseg = (total + pl.seg - 1) / pl.seg;
-
-  void *k0, *k1, *v0, *v1, *bk, *rc, *rk, *rc2, *rk2, *pa, *pb, *tmp;
-  ECG_TRY(ws_get(ctx, "msm_k0", total * 4, &k0));
-  ECG_TRY(ws_get(ctx, "msm_k1", total * 4, &k1));
-  ECG_TRY(ws_get(ctx, "msm_v0", total * 4, &v0));
-  ECG_TRY(ws_get(ctx, "msm_v1", total * 4, &v1));
-  ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nb * sizeof(X), &bk));
-  ECG_TRY(ws_get(ctx, "msm_recs", 2 * nseg * sizeof(X), &rc));
-  ECG_TRY(ws_get(ctx, "msm_rkeys", 2 * nseg * 4, &rk));
-  const size_t nseg1 = (2 * nseg + MSM_COMBINE_SEG - 1) / MSM_COMBINE_SEG;
-  ECG_TRY(ws_get(ctx, "msm_recs2", 2 * nseg1 * sizeof(X), &rc2));
-  ECG_TRY(ws_get(ctx, "msm_rkeys2", 2 * nseg1 * 4, &rk2));
-  ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
-  ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * pl.S / MSM_FOLD + pl.G) * sizeof(X), &pb));
-
-  hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(m, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     (const uint4*)d_scalars, g, pl, (uint32_t*)k0, (uint32_t*)v0);
-  ECG_HIP(hipGetLastError());
-
-  size_t tmp_bytes = 0;
-  ECG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
-                                             (uint32_t*)v1, total, 0, key_bits, s));
-  ECG_TRY(ws_get(ctx, "msm_sort_tmp", tmp_bytes, &tmp));
-  ECG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
-                                             (uint32_t*)v1, total, 0, key_bits, s));
-
-  // buckets nobody writes (no term) stay the identity: all-zero XYZZ (ZZ = 0)
-  ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X), s));
-
-  ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
-  hipLaunchKernelGGL(msm_accumulate_kernel<C>, dim3(blocks_for(nseg, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     (const F*)d_bases, (const uint32_t*)k1, (const uint32_t*)v1, total, sentinel, pl.seg, (X*)bk,
-                     (X*)rc, (uint32_t*)rk);
-  ECG_HIP(hipGetLastError());
-  ECG_TRY(kt_end(ctx, "msm_accumulate", s));
-
-  // combine the segment-edge partials, level by level
-  size_t nrec = 2 * nseg;
-  X* rin = (X*)rc;
-  uint32_t* kin = (uint32_t*)rk;
-  X* rout = (X*)rc2;
-  uint32_t* kout = (uint32_t*)rk2;
-  for (;;) {
-    const bool fin = nrec <= MSM_COMBINE_SEG;
-    const size_t nthr = (nrec + MSM_COMBINE_SEG - 1) / MSM_COMBINE_SEG;
-    hipLaunchKernelGGL(msm_combine_kernel<C>, dim3(blocks_for(nthr, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                       (const X*)rin, (const uint32_t*)kin, nrec, sentinel, MSM_COMBINE_SEG, fin ? 1 : 0, (X*)bk,
-                       rout, kout);
-    ECG_HIP(hipGetLastError());
-    if (fin) break;
-    nrec = 2 * nthr;
-    std::swap(rin, rout);
-    std::swap(kin, kout);
-  }
-
-  hipLaunchKernelGGL(msm_reduce_kernel<C>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
-                     dim3(MSM_THREADS), 0, s, (const X*)bk, pl, (X*)pa);
-  ECG_HIP(hipGetLastError());
-
-  uint32_t cnt = pl.S;
-  X* in = (X*)pa;
-  X* out = (X*)pb;
-  while (cnt > 1) {
-    const uint32_t oc = (cnt + MSM_FOLD - 1) / MSM_FOLD;
-    hipLaunchKernelGGL(msm_sum_kernel<C>, dim3(blocks_for((size_t)pl.G * oc, MSM_THREADS)), dim3(MSM_THREADS),
-                       0, s, (const X*)in, pl.G, cnt, oc, out);
-    ECG_HIP(hipGetLastError());
-    X* t = in;
-    in = out;
-    out = t;
-    cnt = oc;
-  }
-  *d_sums = in;
-  return ECG_OK;
-}
-
-// One MSM, processed in device passes of at most MSM_MAX_CHUNK terms; the
-// window sums come back to the host, which runs the Horner fold.
-template <class C>
-static int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
-                        hipStream_t s, ecg_abort_cb abort_cb, void* user, uint32_t scalar_mont) {
-  using F = typename C::Fq;
-  using X = XYZZ<F>;
-  using HP = typename C::FqParams;
-  using HX = host::HXYZZ<HP>;
-  kt_reset(ctx, "msm_accumulate");
-  HX total_acc = HX::zero();
-  std::vector<X> win;
-  for (size_t off = 0; off < n; off += MSM_MAX_CHUNK) {
-    if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144
-    const size_t m = n - off < MSM_MAX_CHUNK ? n - off : MSM_MAX_CHUNK;
-    const MsmPlan pl = make_plan(m, (uint32_t)C::FrParams::BITS);
-    const MsmGeom g{1, 1, m, m, scalar_mont};
-    void* d_sums;
-    ECG_TRY(msm_core_t<C>(ctx, (const F*)d_bases + 2 * off, (const uint4*)d_scalars + 2 * off, g, pl, s, &d_sums));
-    // window sums -> host; Horner fold over windows (multiexp.rs:221-233)
-    win.resize(pl.W);
-    ECG_HIP(hipMemcpyAsync(win.data(), d_sums, pl.W * sizeof(X), hipMemcpyDeviceToHost, s));
-    ECG_HIP(hipStreamSynchronize(s));
-    HX acc = HX::zero();
-    for (int w = (int)pl.W - 1; w >= 0; w--) {
-      for (uint32_t k = 0; k < pl.c; k++) acc = host::hdbl(acc);
-      HX ww;
-      // device values are in the lazy range [0, 2p]: canonicalise
-      memcpy(ww.X.v, win[w].X.v, sizeof(ww.X.v));
-      memcpy(ww.Y.v, win[w].Y.v, sizeof(ww.Y.v));
-      memcpy(ww.ZZ.v, win[w].ZZ.v, sizeof(ww.ZZ.v));
-      memcpy(ww.ZZZ.v, win[w].ZZZ.v, sizeof(ww.ZZZ.v));
-      ww.X = host::hcanon(ww.X);
-      ww.Y = host::hcanon(ww.Y);
-      ww.ZZ = host::hcanon(ww.ZZ);
-      ww.ZZZ = host::hcanon(ww.ZZZ);
-      acc = host::hadd_pts(acc, ww);
-    }
-    total_acc = host::hadd_pts(total_acc, acc);
-  }
-  host::hto_jac_norm(total_acc, out_jac);
-  return ECG_OK;
 }
 
 int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
@@ -611,49 +28,9 @@ int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scala
     set_error("multiexp: at most 2^31-1 terms per call");
     return ECG_ERR_INVALID;
   }
-  switch (curve_id) {
-    case ECG_CURVE_BLS12_381:
-      return msm_single_t<BLS12_381>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0);
-    case ECG_CURVE_BN254:
-      return msm_single_t<BN254>(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0);
-    default:
-      set_error("multiexp: unknown curve_id %d", curve_id);
-      return ECG_ERR_INVALID;
-  }
-}
-
-// Batched multi-line MSM (ag-cuda-ec multiple_multiexp): all tasks in one
-// pass -- one sort over (task, window, bucket) keys, one accumulation launch,
-// one reduction -- then a device fold per task.  out_jac: tasks x 3 x Fq,
-// line-major (results[line * n_chunks + chunk], multiexp.cl:260).
-template <class C>
-static int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
-                       uint32_t window_bits, uint64_t* out_jac, hipStream_t s) {
-  using F = typename C::Fq;
-  kt_reset(ctx, "msm_accumulate");
-  const uint32_t tasks = g.tasks();
-  const size_t ob = (size_t)tasks * 3 * sizeof(F);
-  if (g.clen == 0) {  // empty chunks: every task is the identity
-    using HX = host::HXYZZ<typename C::FqParams>;
-    for (uint32_t t = 0; t < tasks; t++) host::hto_jac_norm(HX::zero(), out_jac + (size_t)t * 3 * C::FqParams::N);
-    return ECG_OK;
-  }
-  MsmPlan pl = make_plan(g.clen, (uint32_t)C::FrParams::BITS, window_bits);
-  pl.G = tasks * pl.W;
-  if ((uint64_t)pl.G * pl.B >= 0xffffffffull) {
-    set_error("multiple_multiexp: %u tasks x %u windows x %u buckets exceeds the 32-bit bucket space", tasks, pl.W,
-              pl.B);
-    return ECG_ERR_INVALID;
-  }
-  void *d_sums, *d_out;
-  ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums));
-  ECG_TRY(ws_get(ctx, "msm_batch_out", ob, &d_out));
-  hipLaunchKernelGGL(msm_fold_kernel<C>, dim3(blocks_for(tasks, 64)), dim3(64), 0, s, (const XYZZ<F>*)d_sums, pl,
-                     tasks, (F*)d_out);
-  ECG_HIP(hipGetLastError());
-  ECG_HIP(hipMemcpyAsync(out_jac, d_out, ob, hipMemcpyDeviceToHost, s));
-  ECG_HIP(hipStreamSynchronize(s));
-  return ECG_OK;
+  const MsmOps* o = msm_ops(curve_id, "multiexp");
+  if (!o) return ECG_ERR_INVALID;
+  return o->single(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0);
 }
 
 int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const void* d_scalars,
@@ -681,37 +58,20 @@ int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_base
     set_error("multiple_multiexp: %zu tasks is too many", n_lines * n_chunks);
     return ECG_ERR_INVALID;
   }
-  const MsmGeom g{(uint32_t)n_lines, (uint32_t)n_chunks, line_len, line_len / n_chunks, scalar_mont != 0};
-  switch (curve_id) {
-    case ECG_CURVE_BLS12_381: return msm_batch_t<BLS12_381>(ctx, d_bases, d_scalars, g, window_bits, out_jac, s);
-    case ECG_CURVE_BN254: return msm_batch_t<BN254>(ctx, d_bases, d_scalars, g, window_bits, out_jac, s);
-    default:
-      set_error("multiple_multiexp: unknown curve_id %d", curve_id);
-      return ECG_ERR_INVALID;
-  }
-}
-
-template <class C>
-static void point_sum_host_t(const uint64_t* pts, size_t count, uint64_t* out_jac) {
-  using HP = typename C::FqParams;
-  constexpr int N = HP::N;
-  host::HXYZZ<HP> acc = host::HXYZZ<HP>::zero();
-  for (size_t i = 0; i < count; i++) acc = host::hadd_pts(acc, host::hfrom_jac<HP>(&pts[i * 3 * N]));
-  host::hto_jac_norm(acc, out_jac);
+  const MsmOps* o = msm_ops(curve_id, "multiple_multiexp");
+  if (!o) return ECG_ERR_INVALID;
+  return o->batch(ctx, d_bases, d_scalars, (uint32_t)n_lines, (uint32_t)n_chunks, line_len, scalar_mont != 0,
+                  window_bits, out_jac, s);
 }
 
 int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac) {
-  switch (curve_id) {
-    case ECG_CURVE_BLS12_381: point_sum_host_t<BLS12_381>(points, count, out_jac); return ECG_OK;
-    case ECG_CURVE_BN254: point_sum_host_t<BN254>(points, count, out_jac); return ECG_OK;
-    default:
-      set_error("point_sum: unknown curve_id %d", curve_id);
-      return ECG_ERR_INVALID;
-  }
+  const MsmOps* o = msm_ops(curve_id, "point_sum");
+  if (!o) return ECG_ERR_INVALID;
+  return o->point_sum(points, count, out_jac);
 }
 
 int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, uint64_t* out_jac, hipStream_t s) {
-  if (curve_id != ECG_CURVE_BLS12_381 && curve_id != ECG_CURVE_BN254) {
+  if (!curve_valid(curve_id)) {
     set_error("point_sum: unknown curve_id %d", curve_id);
     return ECG_ERR_INVALID;
   }
@@ -722,38 +82,11 @@ int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count
   return point_sum_host(curve_id, pts.data(), count, out_jac);
 }
 
-template <class C>
-static int gen_bases_t(ecg_ctx* ctx, const uint64_t* a, const uint64_t* b, size_t n, void* d_out, hipStream_t s) {
-  using F = typename C::Fq;
-  using S = Fp<typename C::FrParams>;
-  if (n == 0) return ECG_OK;
-  // a, b arrive canonical; the kernels convert to Montgomery themselves.
-  S ac, bc;
-  memcpy(ac.v, a, sizeof(ac.v));
-  memcpy(bc.v, b, sizeof(bc.v));
-  void *q, *scratch;
-  ECG_TRY(ws_get(ctx, "gen_q", 2 * sizeof(F), &q));
-  ECG_TRY(ws_get(ctx, "gen_scratch", n * 3 * sizeof(F), &scratch));
-  hipLaunchKernelGGL(gen_step_kernel<C>, dim3(1), dim3(64), 0, s, bc, (F*)q);
-  ECG_HIP(hipGetLastError());
-  const size_t threads = (n + GEN_BLOCK - 1) / GEN_BLOCK;
-  hipLaunchKernelGGL(gen_bases_kernel<C>, dim3(blocks_for(threads, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     ac, bc, n, (const F*)q, (F*)d_out, (F*)scratch);
-  ECG_HIP(hipGetLastError());
-  ECG_HIP(hipStreamSynchronize(s));
-  ws_release(ctx, "gen_scratch");
-  return ECG_OK;
-}
-
 int gen_bases_run(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n, void* d_out,
                   hipStream_t s) {
-  switch (curve_id) {
-    case ECG_CURVE_BLS12_381: return gen_bases_t<BLS12_381>(ctx, a, b, n, d_out, s);
-    case ECG_CURVE_BN254: return gen_bases_t<BN254>(ctx, a, b, n, d_out, s);
-    default:
-      set_error("gen_bases: unknown curve_id %d", curve_id);
-      return ECG_ERR_INVALID;
-  }
+  const MsmOps* o = msm_ops(curve_id, "gen_bases");
+  if (!o) return ECG_ERR_INVALID;
+  return o->gen_bases(ctx, a, b, n, d_out, s);
 }
 
 }  // namespace ecg

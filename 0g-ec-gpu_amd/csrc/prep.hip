@@ -87,15 +87,13 @@ int bases_from_ark(ecg_ctx* ctx, int curve_id, const void* d_ark, size_t n, void
   (void)ctx;
   if (n == 0) return ECG_OK;
   const dim3 grid((uint32_t)((n + PREP_THREADS - 1) / PREP_THREADS));
-  switch (curve_id) {
-    case ECG_CURVE_BLS12_381:
-      hipLaunchKernelGGL(bases_from_ark_kernel<6>, grid, dim3(PREP_THREADS), 0, s, (const uint64_t*)d_ark, n,
-                         (uint64_t*)d_xy);
-      break;
-    case ECG_CURVE_BN254:
-      hipLaunchKernelGGL(bases_from_ark_kernel<4>, grid, dim3(PREP_THREADS), 0, s, (const uint64_t*)d_ark, n,
-                         (uint64_t*)d_xy);
-      break;
+  const uint64_t* src = (const uint64_t*)d_ark;
+  uint64_t* dst = (uint64_t*)d_xy;
+  switch (fq_limbs64(curve_id)) {  // G2: x, y in Fq2, then the flag (Affine<G2Config>)
+    case 6: hipLaunchKernelGGL(bases_from_ark_kernel<6>, grid, dim3(PREP_THREADS), 0, s, src, n, dst); break;
+    case 4: hipLaunchKernelGGL(bases_from_ark_kernel<4>, grid, dim3(PREP_THREADS), 0, s, src, n, dst); break;
+    case 12: hipLaunchKernelGGL(bases_from_ark_kernel<12>, grid, dim3(PREP_THREADS), 0, s, src, n, dst); break;
+    case 8: hipLaunchKernelGGL(bases_from_ark_kernel<8>, grid, dim3(PREP_THREADS), 0, s, src, n, dst); break;
     default:
       set_error("bases_from_ark: unknown curve_id %d", curve_id);
       return ECG_ERR_INVALID;

@@ -33,11 +33,12 @@ LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libecgpu.so")
 
 # ids shared with include/ecgpu.h
 FIELD_BLS12_381_FR, FIELD_BLS12_381_FQ, FIELD_BN254_FR, FIELD_BN254_FQ = 0, 1, 2, 3
-CURVE_BLS12_381, CURVE_BN254 = 0, 1
+CURVE_BLS12_381, CURVE_BN254, CURVE_BLS12_381_G2, CURVE_BN254_G2 = 0, 1, 2, 3
 FIELD_NAMES = {"bls12_381_fr": 0, "bls12_381_fq": 1, "bn254_fr": 2, "bn254_fq": 3}
-CURVE_NAMES = {"bls12_381": 0, "bn254": 1}
-CURVE_FQ_LIMBS = {0: 6, 1: 4}
-CURVE_FR_FIELD = {0: FIELD_BLS12_381_FR, 1: FIELD_BN254_FR}
+CURVE_NAMES = {"bls12_381": 0, "bn254": 1, "bls12_381_g2": 2, "bn254_g2": 3}
+# u64 words per point coordinate (Fq for G1, Fq2 = [c0, c1] for G2)
+CURVE_FQ_LIMBS = {0: 6, 1: 4, 2: 12, 3: 8}
+CURVE_FR_FIELD = {0: FIELD_BLS12_381_FR, 1: FIELD_BN254_FR, 2: FIELD_BLS12_381_FR, 3: FIELD_BN254_FR}
 FR_TWO_ADICITY = {FIELD_BLS12_381_FR: 32, FIELD_BN254_FR: 28}
 
 ECG_OK, ECG_ABORTED = 0, 1

@@ -16,6 +16,9 @@
  *                    (PrimeFieldRepr::to_bigint, ag-types/src/impls.rs:7-18).
  *   base           : [x, y] Montgomery, identity = all zero
  *                    (GpuRepr::to_gpu_repr, ag-types/src/impls.rs:48-58).
+ *                    G2 coordinates are Fq2 = [c0, c1] (QuadExtField), so a
+ *                    coordinate is Lq = 2 x (Fq limbs): 12 u64 for BLS12-381
+ *                    G2, 8 for BN254 G2.
  *   result point   : Jacobian [X, Y, Z] Montgomery (G::Curve), normalised:
  *                    (x, y, 1) or the identity (0, 1, 0).
  *
@@ -41,6 +44,8 @@ extern "C" {
 
 #define ECG_CURVE_BLS12_381 0 /* G1 over BLS12-381 Fq, scalars in Fr */
 #define ECG_CURVE_BN254 1     /* G1 over BN254 Fq, scalars in Fr      */
+#define ECG_CURVE_BLS12_381_G2 2 /* G2 over BLS12-381 Fq2 (field2.cl), scalars in Fr */
+#define ECG_CURVE_BN254_G2 3     /* G2 over BN254 Fq2, scalars in Fr               */
 
 #define ECG_OK 0
 #define ECG_ABORTED 1

@@ -408,3 +408,126 @@ class Xoshiro256ss:
             v &= (1 << nbits) - 1
             if v < f.modulus:
                 return v
+
+
+# --------------------------------------------------------------------------
+# Fq2 = Fq[u]/(u^2 + 1) (ag-build/cl/field2.cl:1-61; the quadratic extension
+# of both BLS12-381 and BN254) and G2.  Fq2 overloads the int operators the
+# formulas above use (+, -, *, **, % p, == 0, pow(z, -1, p)), so jac_double /
+# jac_add / jac_add_mixed / multiexp_cpu run unchanged over Fq2.
+# --------------------------------------------------------------------------
+
+
+class Fq2:
+    __slots__ = ("c0", "c1", "p")
+
+    def __init__(self, c0: int, c1: int, p: int):
+        self.c0, self.c1, self.p = c0 % p, c1 % p, p
+
+    def _lift(self, o):
+        return o if isinstance(o, Fq2) else Fq2(o, 0, self.p)
+
+    def __add__(self, o):
+        o = self._lift(o)
+        return Fq2(self.c0 + o.c0, self.c1 + o.c1, self.p)
+
+    __radd__ = __add__
+
+    def __sub__(self, o):
+        o = self._lift(o)
+        return Fq2(self.c0 - o.c0, self.c1 - o.c1, self.p)
+
+    def __rsub__(self, o):
+        return self._lift(o) - self
+
+    def __neg__(self):
+        return Fq2(-self.c0, -self.c1, self.p)
+
+    def __mul__(self, o):
+        if isinstance(o, int):
+            return Fq2(self.c0 * o, self.c1 * o, self.p)
+        # (a0 + a1 u)(b0 + b1 u) = a0 b0 - a1 b1 + (a0 b1 + a1 b0) u  (field2.cl:34-47)
+        return Fq2(self.c0 * o.c0 - self.c1 * o.c1, self.c0 * o.c1 + self.c1 * o.c0, self.p)
+
+    __rmul__ = __mul__
+
+    def __mod__(self, _p):
+        return self
+
+    def __pow__(self, e, mod=None):
+        if e < 0:
+            n = (self.c0 * self.c0 + self.c1 * self.c1) % self.p
+            ni = pow(n, -1, self.p)
+            return Fq2(self.c0 * ni, -self.c1 * ni, self.p) ** (-e)
+        r = Fq2(1, 0, self.p)
+        b = self
+        while e:
+            if e & 1:
+                r = r * b
+            b = b * b
+            e >>= 1
+        return r
+
+    def __eq__(self, o):
+        o = self._lift(o)
+        return self.c0 == o.c0 and self.c1 == o.c1
+
+    def __hash__(self):
+        return hash((self.c0, self.c1))
+
+    def __repr__(self):
+        return f"Fq2({hex(self.c0)}, {hex(self.c1)})"
+
+
+@dataclass(frozen=True)
+class CurveG2:
+    name: str
+    fq: Field
+    fr: Field
+    b: tuple  # Fq2 coefficient (c0, c1)
+    gx: tuple
+    gy: tuple
+
+    def fq2(self, c0: int, c1: int = 0) -> Fq2:
+        return Fq2(c0, c1, self.fq.modulus)
+
+    @property
+    def gen(self):
+        return (self.fq2(*self.gx), self.fq2(*self.gy))
+
+
+# Public curve definitions: BLS12-381 G2 (y^2 = x^3 + 4(u + 1)), BN254 G2
+# (y^2 = x^3 + 3/(9 + u), EIP-197 generator).  test_oracle_g2 checks on-curve
+# and r * G2 = O for both before anything uses them.
+BLS12_381_G2 = CurveG2(
+    "bls12_381_g2", BLS12_381_FQ, BLS12_381_FR, (4, 4),
+    (0x024AA2B2F08F0A91260805272DC51051C6E47AD4FA403B02B4510B647AE3D1770BAC0326A805BBEFD48056C8C121BDB8,
+     0x13E02B6052719F607DACD3A088274F65596BD0D09920B61AB5DA61BBDC7F5049334CF11213945D57E5AC7D055D042B7E),
+    (0x0CE5D527727D6E118CC9CDC6DA2E351AADFD9BAA8CBDD3A76D429A695160D12C923AC9CC3BACA289E193548608B82801,
+     0x0606C4A02EA734CC32ACD2B02BC28B99CB3E287E85A763AF267492AB572E99AB3F370D275CEC1DA1AAA9075FF05F79BE))
+_bn_b2 = Fq2(3, 0, BN254_FQ.modulus) * (Fq2(9, 1, BN254_FQ.modulus) ** -1)
+BN254_G2 = CurveG2(
+    "bn254_g2", BN254_FQ, BN254_FR, (_bn_b2.c0, _bn_b2.c1),
+    (10857046999023057135944570762232829481370756359578518086990519993285655852781,
+     11559732032986387107991004021392285783925812861821192530917403151452391805634),
+    (8495653923123431417604973247489272438418190587263600148770280649306958101930,
+     4082367875863433681332203403145435568316851327593401208105741076214120093531))
+CURVES_G2 = {c.name: c for c in (BLS12_381_G2, BN254_G2)}
+
+
+def on_curve_g2(curve: CurveG2, P) -> bool:
+    x, y = P
+    return y * y - x * x * x - curve.fq2(*curve.b) == 0
+
+
+def g2_scalar_mul(curve: CurveG2, P_aff, k: int):
+    return scalar_mul(P_aff, k, curve.fq.modulus)
+
+
+def g2_to_affine(curve: CurveG2, P):
+    return jac_to_affine(P, curve.fq.modulus)
+
+
+def g2_multiexp_cpu(curve: CurveG2, bases, exps, c: int | None = None):
+    """multiexp_cpu over G2 (same restatement, Fq2 coordinates)."""
+    return multiexp_cpu(curve, bases, exps, c)
