@@ -57,6 +57,7 @@ struct ecg_ctx {
   // FFT twiddle-table cache key
   int tw_fid = -1;
   int tw_variant = 0;
+  int tw_full = 0;
   uint32_t tw_log_n = 0;
   uint64_t tw_omega[4] = {0, 0, 0, 0};
   // persistent base cache: converted [x, y] bases keyed by the

@@ -64,7 +64,8 @@ ECG_DEV F twiddle(const F* __restrict__ tw_lo, const F* __restrict__ tw_hi, uint
 // ---------------------------------------------------------------------------
 template <class F, int DEG>
 ECG_DEV void pass_load(const F* __restrict__ x, const F* __restrict__ tw_lo, const F* __restrict__ tw_hi,
-                       const LdsPlanes<F>& U, uint32_t log_n, uint32_t lgp, uint32_t log_g, uint32_t E) {
+                       const F* __restrict__ twf, const LdsPlanes<F>& U, uint32_t log_n, uint32_t lgp,
+                       uint32_t log_g, uint32_t E) {
   const uint32_t G = 1u << log_g;
   const uint64_t t = (1ull << log_n) >> DEG;
   const uint64_t p = 1ull << lgp;
@@ -75,8 +76,13 @@ ECG_DEV void pass_load(const F* __restrict__ x, const F* __restrict__ tw_lo, con
     const uint64_t g = g0 + gi;
     F v = load(&x[g + (uint64_t)i * t]);
     if (lgp != 0) {
-      const uint64_t e = ((g & (p - 1)) * i) << s_tw_log;  // < n
-      if (e != 0) v = fmul(v, twiddle(tw_lo, tw_hi, e));
+      const uint64_t k = g & (p - 1);
+      const uint64_t e = (k * i) << s_tw_log;  // < n
+      if (e != 0) {
+        // full per-pass table twf[i * p + k] (one load, k contiguous across
+        // lanes) or the split tables (two loads + one product)
+        v = fmul(v, twf ? load(&twf[(uint64_t)i * p + k]) : twiddle(tw_lo, tw_hi, e));
+      }
     }
     U.put((gi << DEG) + i, v);
   }
@@ -108,7 +114,7 @@ template <class P, int DEG>
 __global__ void __launch_bounds__(DEG >= 12 ? 1024 : DEG == 11 ? 512 : 256)
     ntt_pass_kernel(const Fp<P>* __restrict__ x, Fp<P>* __restrict__ y, const Fp<P>* __restrict__ pq,
                     uint32_t pq_shift, const Fp<P>* __restrict__ tw_lo, const Fp<P>* __restrict__ tw_hi,
-                    uint32_t log_n, uint32_t lgp, uint32_t log_g) {
+                    const Fp<P>* __restrict__ twf, uint32_t log_n, uint32_t lgp, uint32_t log_g) {
   using F = Fp<P>;
   static_assert(F::L == 8, "NTT tiles assume 32-byte scalar-field elements");
   constexpr uint32_t R = 1u << DEG;
@@ -116,7 +122,7 @@ __global__ void __launch_bounds__(DEG >= 12 ? 1024 : DEG == 11 ? 512 : 256)
   const uint32_t E = R << log_g;
   LdsPlanes<F> U{smem, smem + E};
 
-  pass_load<F, DEG>(x, tw_lo, tw_hi, U, log_n, lgp, log_g, E);
+  pass_load<F, DEG>(x, tw_lo, tw_hi, twf, U, log_n, lgp, log_g, E);
   __syncthreads();
 
   // radix-2^2 steps: rounds r and r+1 of the DIF network on quartets
@@ -170,13 +176,13 @@ template <class P, int DEG>
 __global__ void __launch_bounds__(256)
     ntt_pass_v1_kernel(const Fp<P>* __restrict__ x, Fp<P>* __restrict__ y, const Fp<P>* __restrict__ pq,
                        uint32_t pq_shift, const Fp<P>* __restrict__ tw_lo, const Fp<P>* __restrict__ tw_hi,
-                       uint32_t log_n, uint32_t lgp, uint32_t log_g) {
+                       const Fp<P>* __restrict__ twf, uint32_t log_n, uint32_t lgp, uint32_t log_g) {
   using F = Fp<P>;
   constexpr uint32_t R = 1u << DEG;
   extern __shared__ uint4 smem[];
   const uint32_t E = R << log_g;
   LdsPlanes<F> U{smem, smem + E};
-  pass_load<F, DEG>(x, tw_lo, tw_hi, U, log_n, lgp, log_g, E);
+  pass_load<F, DEG>(x, tw_lo, tw_hi, twf, U, log_n, lgp, log_g, E);
   __syncthreads();
 #pragma unroll 1
   for (int rnd = 0; rnd < DEG; rnd++) {
@@ -195,6 +201,18 @@ __global__ void __launch_bounds__(256)
     __syncthreads();
   }
   pass_store<F, DEG>(y, U, lgp, log_g, E);
+}
+
+// Full inter-pass twiddle table of one pass: out[i * p + k] = w^((k i) << s),
+// i < 2^deg, k < p = 2^lgp, s = log n - lgp - deg.
+template <class P>
+__global__ void ntt_fulltw_kernel(const Fp<P>* __restrict__ tw_lo, const Fp<P>* __restrict__ tw_hi, uint32_t lgp,
+                                  uint32_t deg, uint32_t log_n, Fp<P>* __restrict__ out) {
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >> (lgp + deg)) return;
+  const uint64_t k = idx & ((1ull << lgp) - 1), i = idx >> lgp;
+  const uint64_t e = (k * i) << (log_n - lgp - deg);
+  store(&out[idx], e ? twiddle(tw_lo, tw_hi, e) : Fp<P>::one());
 }
 
 // out[j] = w^(j << shift), j < count  (w given by value, Montgomery)
@@ -224,6 +242,7 @@ struct PassArgs {
   uint32_t pq_shift;
   const void* tw_lo;
   const void* tw_hi;
+  const void* twf;  // full table of this pass, or null
   uint32_t log_n, lgp;
 };
 
@@ -253,7 +272,7 @@ static hipError_t launch_pass(const PassArgs& a, hipStream_t s) {
     attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(threads), lds, s, (const F*)a.x, (F*)a.y, (const F*)a.pq,
-                     a.pq_shift, (const F*)a.tw_lo, (const F*)a.tw_hi, a.log_n, a.lgp, log_g);
+                     a.pq_shift, (const F*)a.tw_lo, (const F*)a.tw_hi, (const F*)a.twf, a.log_n, a.lgp, log_g);
   return hipGetLastError();
 }
 
@@ -280,6 +299,14 @@ static int ntt_variant() {
   static int v = [] {
     const char* e = getenv("ECG_NTT_VARIANT");
     return (e && e[0] == '1') ? 1 : 2;
+  }();
+  return v;
+}
+
+static bool ntt_full_twiddles() {  // per-pass full twiddle tables (A/B: ECG_NTT_FULLTW=0)
+  static bool v = [] {
+    const char* e = getenv("ECG_NTT_FULLTW");
+    return !(e && e[0] == '0');
   }();
   return v;
 }
@@ -336,8 +363,31 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
   F* tw_lo = pq + pq_cnt;
   F* tw_hi = tw_lo + lo_cnt;
 
+  // full per-pass tables (passes after the first): sum of 2^(lgp + deg) <= 2n entries
+  const bool full = ntt_full_twiddles() && log_n <= 28 && np > 1;
+  F* twf[40] = {nullptr};
+  if (full) {
+    uint64_t tot = 0;
+    uint32_t lg = 0;
+    for (int k = 0; k < np; k++) {
+      if (k > 0) tot += 1ull << (lg + degs[k]);
+      lg += degs[k];
+    }
+    void* t;
+    ECG_TRY(ws_get(ctx, "ntt_twf", tot * sizeof(F), &t));
+    uint64_t off = 0;
+    lg = 0;
+    for (int k = 0; k < np; k++) {
+      if (k > 0) {
+        twf[k] = (F*)t + off;
+        off += 1ull << (lg + degs[k]);
+      }
+      lg += degs[k];
+    }
+  }
+
   const bool cached = ctx->tw_fid == field_id && ctx->tw_log_n == log_n && ctx->tw_variant == variant &&
-                      memcmp(ctx->tw_omega, omega, sizeof(ctx->tw_omega)) == 0;
+                      ctx->tw_full == (int)full && memcmp(ctx->tw_omega, omega, sizeof(ctx->tw_omega)) == 0;
   if (!cached) {
     F w;
     memcpy(w.v, omega, sizeof(w.v));
@@ -348,10 +398,22 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
                        lo_cnt, tw_lo);
     hipLaunchKernelGGL(ntt_powers_kernel<P>, dim3((uint32_t)((hi_cnt + 255) / 256)), dim3(256), 0, s, w,
                        (uint32_t)NTT_LO_BITS, hi_cnt, tw_hi);
+    if (full) {
+      uint32_t lg = 0;
+      for (int k = 0; k < np; k++) {
+        if (k > 0) {
+          const uint64_t cnt = 1ull << (lg + degs[k]);
+          hipLaunchKernelGGL(ntt_fulltw_kernel<P>, dim3((uint32_t)((cnt + 255) / 256)), dim3(256), 0, s, tw_lo,
+                             tw_hi, lg, degs[k], log_n, twf[k]);
+        }
+        lg += degs[k];
+      }
+    }
     ECG_HIP(hipGetLastError());
     ctx->tw_fid = field_id;
     ctx->tw_log_n = log_n;
     ctx->tw_variant = variant;
+    ctx->tw_full = (int)full;
     memcpy(ctx->tw_omega, omega, sizeof(ctx->tw_omega));
   }
 
@@ -376,7 +438,7 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
     if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // fft.rs:94-98
     src = bufs[k];
     dst = bufs[k + 1];
-    const PassArgs a{src, dst, pq, max_deg - degs[k], tw_lo, tw_hi, log_n, lgp};
+    const PassArgs a{src, dst, pq, max_deg - degs[k], tw_lo, tw_hi, twf[k], log_n, lgp};
     ECG_TRY(kt_begin(ctx, "ntt_pass", s));
     hipError_t e = variant == 1 ? launch_pass_deg<P, true>((int)degs[k], a, s)
                                 : launch_pass_deg<P, false>((int)degs[k], a, s);
