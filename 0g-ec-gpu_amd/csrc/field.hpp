@@ -74,10 +74,18 @@ struct Fp {
 // Carry-chain primitives
 // ---------------------------------------------------------------------------
 
+// The asm statements touch only their operands, so they are not volatile:
+// the scheduler may then interleave independent products (measured: the
+// 2^24 NTT runs 7% faster than with volatile, which pins program order).
+// -DECG_ASM_QUAL=volatile restores the pinned form for A/B.
+#ifndef ECG_ASM_QUAL
+#define ECG_ASM_QUAL
+#endif
+
 // acc(96) += a * b   : v_mad_u64_u32 with carry-out + v_addc into top.
 ECG_DEV void mac96(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
   uint64_t cc;
-  asm volatile(
+  asm ECG_ASM_QUAL(
       "v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
       "v_addc_co_u32 %2, %1, %2, 0, %1"
       : "+v"(acc), "=&s"(cc), "+v"(top)
@@ -87,7 +95,7 @@ ECG_DEV void mac96(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
 // Same with b a wave-uniform (SGPR) operand (modulus limbs).
 ECG_DEV void mac96s(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b_uniform) {
   uint64_t cc;
-  asm volatile(
+  asm ECG_ASM_QUAL(
       "v_mad_u64_u32 %0, %1, %3, %4, %0\n\t"
       "v_addc_co_u32 %2, %1, %2, 0, %1"
       : "+v"(acc), "=&s"(cc), "+v"(top)
@@ -105,7 +113,7 @@ ECG_DEV uint32_t mont_digit(uint32_t lo) {
     return 0u - lo;
   } else {
     uint64_t r, cc;
-    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cc) : "v"(lo), "s"(inv));
+    asm ECG_ASM_QUAL("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cc) : "v"(lo), "s"(inv));
     return (uint32_t)r;
   }
 }
@@ -198,21 +206,21 @@ ECG_DEV bool feq(const Fp<P>& a, const Fp<P>& b) {
   "v_addc_co_u32 %2, %1, %2, 0, %1\n\t"
 ECG_DEV void mac96x2(uint64_t& acc, uint32_t& top, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1) {
   uint64_t cc;
-  asm volatile(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6")
+  asm ECG_ASM_QUAL(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6")
                : "+v"(acc), "=&s"(cc), "+v"(top)
                : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
 }
 ECG_DEV void mac96x3(uint64_t& acc, uint32_t& top, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1,
                      uint32_t a2, uint32_t b2) {
   uint64_t cc;
-  asm volatile(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6") ECG_MAC_STEP("%7", "%8")
+  asm ECG_ASM_QUAL(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6") ECG_MAC_STEP("%7", "%8")
                : "+v"(acc), "=&s"(cc), "+v"(top)
                : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2));
 }
 ECG_DEV void mac96x4(uint64_t& acc, uint32_t& top, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1,
                      uint32_t a2, uint32_t b2, uint32_t a3, uint32_t b3) {
   uint64_t cc;
-  asm volatile(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6") ECG_MAC_STEP("%7", "%8")
+  asm ECG_ASM_QUAL(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6") ECG_MAC_STEP("%7", "%8")
                    ECG_MAC_STEP("%9", "%10")
                : "+v"(acc), "=&s"(cc), "+v"(top)
                : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3));
@@ -220,21 +228,21 @@ ECG_DEV void mac96x4(uint64_t& acc, uint32_t& top, uint32_t a0, uint32_t b0, uin
 // ... and with the second operand wave-uniform (modulus limbs in SGPRs).
 ECG_DEV void mac96x2s(uint64_t& acc, uint32_t& top, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1) {
   uint64_t cc;
-  asm volatile(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6")
+  asm ECG_ASM_QUAL(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6")
                : "+v"(acc), "=&s"(cc), "+v"(top)
                : "v"(a0), "s"(b0), "v"(a1), "s"(b1));
 }
 ECG_DEV void mac96x3s(uint64_t& acc, uint32_t& top, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1,
                       uint32_t a2, uint32_t b2) {
   uint64_t cc;
-  asm volatile(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6") ECG_MAC_STEP("%7", "%8")
+  asm ECG_ASM_QUAL(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6") ECG_MAC_STEP("%7", "%8")
                : "+v"(acc), "=&s"(cc), "+v"(top)
                : "v"(a0), "s"(b0), "v"(a1), "s"(b1), "v"(a2), "s"(b2));
 }
 ECG_DEV void mac96x4s(uint64_t& acc, uint32_t& top, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1,
                       uint32_t a2, uint32_t b2, uint32_t a3, uint32_t b3) {
   uint64_t cc;
-  asm volatile(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6") ECG_MAC_STEP("%7", "%8")
+  asm ECG_ASM_QUAL(ECG_MAC_STEP("%3", "%4") ECG_MAC_STEP("%5", "%6") ECG_MAC_STEP("%7", "%8")
                    ECG_MAC_STEP("%9", "%10")
                : "+v"(acc), "=&s"(cc), "+v"(top)
                : "v"(a0), "s"(b0), "v"(a1), "s"(b1), "v"(a2), "s"(b2), "v"(a3), "s"(b3));

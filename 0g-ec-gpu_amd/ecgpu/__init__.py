@@ -29,7 +29,8 @@ from typing import Callable, Optional, Sequence
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libecgpu.so")
+# ECGPU_LIB selects another in-tree build of the same library (A/B of build flags)
+LIB_PATH = os.environ.get("ECGPU_LIB") or os.path.join(os.path.dirname(_PKG), "lib", "libecgpu.so")
 
 # ids shared with include/ecgpu.h
 FIELD_BLS12_381_FR, FIELD_BLS12_381_FQ, FIELD_BN254_FR, FIELD_BN254_FQ = 0, 1, 2, 3

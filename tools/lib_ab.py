@@ -1,0 +1,62 @@
+"""A/B of two in-tree builds of libecgpu (dev tool): each library runs in its
+own subprocess (ECGPU_LIB), interleaved over rounds.  Times the 2^26 MSM, the
+2^24 NTT and a 2^14 EC-FFT with device-resident inputs.
+Usage: python tools/lib_ab.py <lib.so> [<lib.so> ...]"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CODE = r'''
+import sys, time, json, numpy as np
+sys.path.insert(0, "%s/0g-ec-gpu_amd")
+import ecgpu
+prog = ecgpu.program(ecgpu.Device(0))
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+res = {}
+n = 1 << 26
+rng = np.random.default_rng(7)
+E = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64); E[:, 3] &= np.uint64(2**62 - 1)
+d_e = ecgpu.DeviceBuffer.upload(prog, E)
+d_b = ecgpu.gen_bases_dev(prog, "bls12_381", 12345, 678910, n)
+ref = ecgpu.msm_dev(prog, "bls12_381", d_b, d_e, n)
+best = 1e9
+for _ in range(4):
+    t = time.perf_counter(); out = ecgpu.msm_dev(prog, "bls12_381", d_b, d_e, n); best = min(best, time.perf_counter() - t)
+res["msm_ms"] = best * 1e3
+res["msm_acc_ms"] = prog.kernel_time("msm_accumulate")[0]
+d_b.free(); d_e.free()
+def omega(ln):
+    w = pow(7, (R - 1) >> 32, R)
+    for _ in range(ln, 32): w = w * w %% R
+    x = w * (1 << 256) %% R
+    return np.array([(x >> (64 * i)) & (2**64 - 1) for i in range(4)], dtype=np.uint64)
+ln = 24
+a = rng.integers(0, 2**64, size=(1 << ln, 4), dtype=np.uint64); a[:, 3] &= np.uint64(2**62 - 1)
+d = ecgpu.DeviceBuffer.upload(prog, a)
+om = omega(ln)
+ecgpu.fft_dev(prog, "bls12_381_fr", d, om, ln)
+best = 1e9
+for _ in range(6):
+    t = time.perf_counter(); ecgpu.fft_dev(prog, "bls12_381_fr", d, om, ln); best = min(best, time.perf_counter() - t)
+res["ntt_ms"] = best * 1e3
+res["ntt_kernel_ms"] = prog.kernel_time("ntt_pass")[0]
+d.free()
+le = 14
+pts = ecgpu.gen_bases_dev(prog, "bls12_381", 3, 7, 1 << le).read(shape=(1 << le, 12))
+one = np.array([((1 << 384) %% int("1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab", 16) >> (64 * i)) & (2**64 - 1) for i in range(6)], dtype=np.uint64)
+jac = np.ascontiguousarray(np.concatenate([pts, np.tile(one, (1 << le, 1))], axis=1))
+dj = ecgpu.DeviceBuffer.upload(prog, jac)
+ome = omega(le)
+ecgpu.ec_fft_dev(prog, "bls12_381", dj, ome, le)
+dj.write(jac)
+t = time.perf_counter(); ecgpu.ec_fft_dev(prog, "bls12_381", dj, ome, le); res["ecfft14_ms"] = (time.perf_counter() - t) * 1e3
+print(json.dumps(res))
+''' % ROOT
+libs = sys.argv[1:]
+for rnd in range(2):
+    for lib in libs:
+        env = dict(os.environ, ECGPU_LIB=os.path.abspath(lib))
+        out = subprocess.run([sys.executable, "-c", CODE], env=env, capture_output=True, text=True, timeout=900)
+        print(rnd, lib, out.stdout.strip()[-400:], out.stderr.strip()[-500:] if out.returncode else "", flush=True)
