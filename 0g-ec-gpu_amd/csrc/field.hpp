@@ -363,6 +363,58 @@ ECG_DEV Fp<P> fmul(const Fp<P>& a, const Fp<P>& b) {
   return r;
 }
 
+// Two-chain form (A/B variant): each column's a*b and m*p products accumulate
+// in two independent 96-bit chains merged before the Montgomery digit.
+// Measured ~12% SLOWER than fmul at every occupancy, 1..8 waves/SIMD
+// (profiles/r01/field_bench_ilp2.log): the product is issue-bound on
+// v_mad_u64_u32 + v_addc, not latency-bound, so extra merge ops only cost.
+ECG_DEV void add96(uint64_t& acc, uint32_t& top, uint64_t acc2, uint32_t top2) {
+  const uint64_t s = acc + acc2;
+  top += top2 + (s < acc ? 1u : 0u);
+  acc = s;
+}
+
+template <class P, bool REDUCE = true>
+ECG_DEV Fp<P> fmul_ilp(const Fp<P>& a, const Fp<P>& b) {
+  constexpr int L = Fp<P>::L;
+  uint32_t m[L];
+  Fp<P> r;
+  uint64_t acc = 0;
+  uint32_t top = 0;
+#pragma unroll
+  for (int k = 0; k < L; k++) {
+    uint64_t acc2 = 0;
+    uint32_t top2 = 0;
+#pragma unroll
+    for (int i = 0; i <= k; i++) {
+      mac96(acc, top, a.v[i], b.v[k - i]);
+      if (i < k) mac96s(acc2, top2, m[i], Fp<P>::p32(k - i));
+    }
+    add96(acc, top, acc2, top2);
+    m[k] = mont_digit<P>((uint32_t)acc);
+    mac96s(acc, top, m[k], Fp<P>::p32(0));
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+#pragma unroll
+  for (int k = L; k < 2 * L - 1; k++) {
+    uint64_t acc2 = 0;
+    uint32_t top2 = 0;
+#pragma unroll
+    for (int i = k - L + 1; i < L; i++) {
+      mac96(acc, top, a.v[i], b.v[k - i]);
+      mac96s(acc2, top2, m[i], Fp<P>::p32(k - i));
+    }
+    add96(acc, top, acc2, top2);
+    r.v[k - L] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)top << 32);
+    top = 0;
+  }
+  r.v[L - 1] = (uint32_t)acc;
+  if constexpr (REDUCE) reduce_once(r);
+  return r;
+}
+
 template <class P>
 ECG_DEV Fp<P> fsqr(const Fp<P>& a) { return fmul(a, a); }
 

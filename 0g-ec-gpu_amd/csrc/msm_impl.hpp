@@ -203,8 +203,16 @@ __global__ void __launch_bounds__(MSM_THREADS)
 // holes.  msm_combine_kernel sums the records level by level.
 constexpr uint32_t KEY_END = 0xffffffffu;
 
+// Occupancy hint for the accumulate kernel (A/B: -DECG_ACC_WAVES=n sets
+// amdgpu_waves_per_eu(n), i.e. a VGPR budget of 512/n per lane).
+#ifdef ECG_ACC_WAVES
+#define ECG_ACC_ATTR __attribute__((amdgpu_waves_per_eu(ECG_ACC_WAVES, ECG_ACC_WAVES)))
+#else
+#define ECG_ACC_ATTR
+#endif
+
 template <class C>
-__global__ void __launch_bounds__(MSM_THREADS)
+__global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
     msm_accumulate_kernel(const typename C::Fq* __restrict__ bases, const uint32_t* __restrict__ keys,
                           const uint32_t* __restrict__ vals, size_t total, uint32_t sentinel, uint32_t seg,
                           XYZZ<typename C::Fq>* __restrict__ buckets, XYZZ<typename C::Fq>* __restrict__ recs,

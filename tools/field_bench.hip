@@ -29,7 +29,8 @@ __global__ void k_chain(const F* x, const F* y, F* out, int n) {
   for (int k = 0; k < CH; k++) a[k] = load(&x[(t + k) % n]);
   for (int i = 0; i < ITERS; i++) {
 #pragma unroll
-    for (int k = 0; k < CH; k++) a[k] = V == 0 ? fmul(a[k], b) : V == 1 ? fmul_cios(a[k], b) : fmul_x4(a[k], b);
+    for (int k = 0; k < CH; k++)
+      a[k] = V == 0 ? fmul(a[k], b) : V == 1 ? fmul_cios(a[k], b) : V == 2 ? fmul_x4(a[k], b) : fmul_ilp(a[k], b);
   }
   F r = a[0];
   for (int k = 1; k < CH; k++) r = fadd(r, a[k]);
@@ -38,13 +39,13 @@ __global__ void k_chain(const F* x, const F* y, F* out, int n) {
 
 // Same chain, but one chain per thread and occupancy forced by dynamic LDS:
 // waves/SIMD = 8 / (blocks of 256 per CU limited by LDS).
-template <class F>
+template <class F, int V>
 __global__ void k_chain_occ(const F* x, const F* y, F* out, int n) {
   extern __shared__ uint32_t lds_pad[];
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   F a = load(&x[t]), b = load(&y[t]);
-  for (int i = 0; i < ITERS; i++) a = fmul(a, b);
+  for (int i = 0; i < ITERS; i++) a = V == 3 ? fmul_ilp(a, b) : fmul(a, b);
   if (threadIdx.x == 1023) lds_pad[0] = a.v[0];  // keep the LDS allocation
   store(&out[t], a);
 }
@@ -57,6 +58,7 @@ __global__ void k_once(const F* x, const F* y, F* o0, F* o1, int n) {
   store(&o0[t], fmul(a, b));
   store(&o1[t], fmul_cios(a, b));
   if (!feq(fmul_x4(a, b), fmul_cios(a, b))) o1[t].v[0] ^= 1;
+  if (!feq(fmul_ilp(a, b), fmul_cios(a, b))) o1[t].v[1] ^= 1;
 }
 
 typedef void (*orc_fmul_t)(int, uint64_t*, const uint64_t*, const uint64_t*);
@@ -101,36 +103,43 @@ static void bench(const char* name, int fid, orc_fmul_t orc) {
   printf("%s correctness: %s (%d mismatches)\n", name, bad ? "FAIL" : "ok", bad);
   hipEvent_t a, b;
   CHK(hipEventCreate(&a)); CHK(hipEventCreate(&b));
-  float best[3] = {1e30f, 1e30f, 1e30f};
+  float best[4] = {1e30f, 1e30f, 1e30f, 1e30f};
   for (int rep = 0; rep < 6; rep++) {
-    for (int v = 0; v < 3; v++) {  // interleaved rounds: A/B in one process
+    for (int v = 0; v < 4; v++) {  // interleaved rounds: A/B in one process
       CHK(hipEventRecord(a));
       if (v == 0) k_chain<F, 0><<<n / 256, 256>>>(dx, dy, d0, n);
       else if (v == 1) k_chain<F, 1><<<n / 256, 256>>>(dx, dy, d1, n);
-      else k_chain<F, 2><<<n / 256, 256>>>(dx, dy, d1, n);
+      else if (v == 2) k_chain<F, 2><<<n / 256, 256>>>(dx, dy, d1, n);
+      else k_chain<F, 3><<<n / 256, 256>>>(dx, dy, d1, n);
       CHK(hipEventRecord(b));
       CHK(hipEventSynchronize(b));
       float ms; CHK(hipEventElapsedTime(&ms, a, b));
       if (ms < best[v]) best[v] = ms;
     }
   }
-  for (int v = 0; v < 3; v++) {
+  for (int v = 0; v < 4; v++) {
     double muls = (double)n * ITERS * CH;
-    printf("  %-6s %s: %8.3f ms  %8.2f G mul/s\n", name, v == 0 ? "fips-asm-x1" : v == 1 ? "cios-c++" : "fips-asm-x4", best[v], muls / best[v] / 1e6);
+    printf("  %-6s %s: %8.3f ms  %8.2f G mul/s\n", name,
+           v == 0 ? "fips-asm-x1" : v == 1 ? "cios-c++" : v == 2 ? "fips-asm-x4" : "fips-ilp2", best[v],
+           muls / best[v] / 1e6);
   }
   // throughput vs occupancy (1 chain per thread): LDS per 256-thread block sets blocks/CU
   for (int wps : {1, 2, 3, 4, 8}) {
     size_t lds = wps >= 8 ? 0 : (160 * 1024) / wps - 256;  // blocks per CU = wps (each block = 1 wave/SIMD)
-    float best = 1e30f;
+    float bst[2] = {1e30f, 1e30f};
     for (int rep = 0; rep < 3; rep++) {
-      CHK(hipEventRecord(a));
-      hipLaunchKernelGGL(k_chain_occ<F>, dim3(n / 256), dim3(256), lds, 0, dx, dy, d0, n);
-      CHK(hipEventRecord(b));
-      CHK(hipEventSynchronize(b));
-      float ms; CHK(hipEventElapsedTime(&ms, a, b));
-      if (ms < best) best = ms;
+      for (int v = 0; v < 2; v++) {
+        CHK(hipEventRecord(a));
+        if (v == 0) hipLaunchKernelGGL((k_chain_occ<F, 0>), dim3(n / 256), dim3(256), lds, 0, dx, dy, d0, n);
+        else hipLaunchKernelGGL((k_chain_occ<F, 3>), dim3(n / 256), dim3(256), lds, 0, dx, dy, d0, n);
+        CHK(hipEventRecord(b));
+        CHK(hipEventSynchronize(b));
+        float ms; CHK(hipEventElapsedTime(&ms, a, b));
+        if (ms < bst[v]) bst[v] = ms;
+      }
     }
-    printf("  %-6s occupancy %d wave(s)/SIMD: %8.2f G mul/s\n", name, wps, (double)n * ITERS / best / 1e6);
+    printf("  %-6s occupancy %d wave(s)/SIMD: fips %8.2f  ilp2 %8.2f G mul/s\n", name, wps,
+           (double)n * ITERS / bst[0] / 1e6, (double)n * ITERS / bst[1] / 1e6);
   }
   CHK(hipFree(dx)); CHK(hipFree(dy)); CHK(hipFree(d0)); CHK(hipFree(d1));
 }
