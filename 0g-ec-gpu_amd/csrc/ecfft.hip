@@ -13,7 +13,13 @@
 // NTT needs buys nothing.  The layout is instead the one that maximises
 // independent lanes per launch:
 //   1. ecfft_load      Jacobian (any Z) -> XYZZ, written to bit-reversed slots
-//   2. ecfft_twiddle   omega^i, i < n/2, canonical (scalar-mul bit source)
+//   2. ecfft_twiddle   omega^i, i < n/2, canonical (scalar-mul bit source); on
+//                      BLS12-381 G1 split into GLV halves k = k1 + k2 LAMBDA
+//                      (phi(x, y) = (BETA x, y) = LAMBDA P on G1): the twiddle
+//                      product becomes a joint 128-bit ladder over
+//                      {P, phi P, P + phi P} -- half the doublings.  Inputs
+//                      must be G1 (prime-order subgroup) points, as ark's
+//                      G1Projective values are.
 //   3. ecfft_stage     log_n launches of n/2 independent radix-2 DIT
 //                      butterflies (A, B) -> (A + wB, A - wB), lazy [0, 2p]
 //                      Fq arithmetic, w = 1 butterflies skip the multiply
@@ -43,14 +49,98 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
 }
 
 template <class C>
+constexpr bool has_glv() {
+  return C::EXT == 1 && C::Gen::GLV != 0;
+}
+
+// GLV split of a canonical scalar k < r (BLS12-381 G1): k = k2 * LAMBDA + k1,
+// 0 <= k1 < LAMBDA < 2^128, k2 < r / LAMBDA < 2^128 (bit-serial division by
+// the fixed 128-bit LAMBDA; runs once per twiddle when the table is built).
+template <class C>
+ECG_DEV void glv_split(const uint32_t* k, uint32_t* k1, uint32_t* k2) {
+  uint32_t lam[5];
+#pragma unroll
+  for (int i = 0; i < 4; i++) lam[i] = (i & 1) ? (uint32_t)(C::Gen::LAMBDA[i >> 1] >> 32) : (uint32_t)C::Gen::LAMBDA[i >> 1];
+  lam[4] = 0;
+  uint32_t rem[5] = {0, 0, 0, 0, 0};
+  uint32_t q[4] = {0, 0, 0, 0};
+  for (int b = 255; b >= 0; b--) {
+#pragma unroll
+    for (int i = 4; i > 0; i--) rem[i] = (rem[i] << 1) | (rem[i - 1] >> 31);
+    rem[0] = (rem[0] << 1) | ((k[b >> 5] >> (b & 31)) & 1);
+    bool ge = true;  // rem >= lam ?
+#pragma unroll
+    for (int i = 4; i >= 0; i--) {
+      if (rem[i] != lam[i]) {
+        ge = rem[i] > lam[i];
+        break;
+      }
+    }
+    if (ge) {
+      uint32_t br = 0;
+#pragma unroll
+      for (int i = 0; i < 5; i++) {
+        const uint64_t d = (uint64_t)rem[i] - lam[i] - br;
+        rem[i] = (uint32_t)d;
+        br = (uint32_t)(d >> 63);
+      }
+      if (b < 128) q[b >> 5] |= 1u << (b & 31);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    k1[i] = rem[i];
+    k2[i] = q[i];
+  }
+}
+
+// Twiddle table entry i (2 x uint4): canonical omega^i, or its GLV halves
+// (k1 | k2) for curves with the endomorphism.
+template <class C>
 __global__ void __launch_bounds__(ECFFT_THREADS)
     ecfft_twiddle_kernel(Fp<typename C::FrParams> omega, uint32_t half, uint4* __restrict__ tw) {
   using S = Fp<typename C::FrParams>;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= half) return;
   S w = from_mont(fpow_u32(omega, i));
-  tw[2 * i] = make_uint4(w.v[0], w.v[1], w.v[2], w.v[3]);
-  tw[2 * i + 1] = make_uint4(w.v[4], w.v[5], w.v[6], w.v[7]);
+  if constexpr (has_glv<C>()) {
+    uint32_t k1[4], k2[4];
+    glv_split<C>(w.v, k1, k2);
+    tw[2 * i] = make_uint4(k1[0], k1[1], k1[2], k1[3]);
+    tw[2 * i + 1] = make_uint4(k2[0], k2[1], k2[2], k2[3]);
+  } else {
+    tw[2 * i] = make_uint4(w.v[0], w.v[1], w.v[2], w.v[3]);
+    tw[2 * i + 1] = make_uint4(w.v[4], w.v[5], w.v[6], w.v[7]);
+  }
+}
+
+// k1 P + k2 phi(P) by a joint (Straus-Shamir) double-and-add over the 128-bit
+// halves: one doubling per bit of the longer half and one full add from the
+// table {P, phi P, P + phi P} per nonzero bit pair.  The table lives in a
+// per-butterfly global slot (L2-resident), keeping VGPRs for the chain.
+template <class C>
+ECG_DEV XYZZ<typename C::Fq> glv_joint_mul(const XYZZ<typename C::Fq>& P, const uint32_t* k1, const uint32_t* k2,
+                                           XYZZ<typename C::Fq>* tab) {
+  using F = typename C::Fq;
+  if (xyzz_is_zero<F, true>(P)) return P;
+  F beta;
+  from_u64_words(beta, C::Gen::BETA);
+  XYZZ<F> phi = P;
+  phi.X = fmul_lz(P.X, beta);
+  store_xyzz(&tab[0], P);
+  store_xyzz(&tab[1], phi);
+  store_xyzz(&tab[2], xyzz_add<F, true>(P, phi));
+  int top = 127;
+  while (top >= 0 && !(((k1[top >> 5] | k2[top >> 5]) >> (top & 31)) & 1)) top--;
+  if (top < 0) return xyzz_zero<F>();
+  const uint32_t d0 = ((k1[top >> 5] >> (top & 31)) & 1) | (((k2[top >> 5] >> (top & 31)) & 1) << 1);
+  XYZZ<F> acc = load_xyzz(&tab[d0 - 1]);
+  for (int b = top - 1; b >= 0; b--) {
+    acc = xyzz_dbl<F, true>(acc);
+    const uint32_t d = ((k1[b >> 5] >> (b & 31)) & 1) | (((k2[b >> 5] >> (b & 31)) & 1) << 1);
+    if (d) acc = xyzz_add<F, true>(acc, load_xyzz(&tab[d - 1]));
+  }
+  return acc;
 }
 
 // Stage s of the DIT: half-size h = 2^s; butterfly t pairs i0 = (t >> s) *
@@ -59,7 +149,7 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
 template <class C>
 __global__ void __launch_bounds__(ECFFT_THREADS)
     ecfft_stage_kernel(XYZZ<typename C::Fq>* __restrict__ a, const uint4* __restrict__ tw, uint32_t log_n,
-                       uint32_t s) {
+                       uint32_t s, XYZZ<typename C::Fq>* __restrict__ glv_tab) {
   using F = typename C::Fq;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (1u << (log_n - 1))) return;
@@ -71,8 +161,13 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
   if (j != 0) {
     const uint32_t e = j << (log_n - 1 - s);
     const uint4 lo = tw[2 * e], hi = tw[2 * e + 1];
-    const uint32_t k[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    B = xyzz_mul_scalar<F, true>(B, k);
+    if constexpr (has_glv<C>()) {
+      const uint32_t k1[4] = {lo.x, lo.y, lo.z, lo.w}, k2[4] = {hi.x, hi.y, hi.z, hi.w};
+      B = glv_joint_mul<C>(B, k1, k2, glv_tab + 3 * (size_t)t);
+    } else {
+      const uint32_t k[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      B = xyzz_mul_scalar<F, true>(B, k);
+    }
   }
   store_xyzz(&a[i0], xyzz_add<F, true>(A, B));
   store_xyzz(&a[i1], xyzz_add<F, true>(A, xyzz_neg<F, true>(B)));
@@ -100,9 +195,10 @@ static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t lo
   using F = typename C::Fq;
   using S = Fp<typename C::FrParams>;
   const uint32_t n = 1u << log_n;
-  void *a, *tw;
+  void *a, *tw, *gt = nullptr;
   ECG_TRY(ws_get(ctx, "ecfft_pts", (size_t)n * sizeof(XYZZ<F>), &a));
   ECG_TRY(ws_get(ctx, "ecfft_tw", (size_t)(n / 2 + 1) * 32, &tw));
+  if (has_glv<C>()) ECG_TRY(ws_get(ctx, "ecfft_glv", (size_t)(n / 2 + 1) * 3 * sizeof(XYZZ<F>), &gt));
   S om;
   memcpy(om.v, omega, sizeof(om.v));
   hipLaunchKernelGGL(ecfft_load_kernel<C>, dim3(ecfft_blocks(n)), dim3(ECFFT_THREADS), 0, s, (const F*)d_jac, log_n,
@@ -121,7 +217,7 @@ static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t lo
     }
     ECG_TRY(kt_begin(ctx, "ecfft_stage", s));
     hipLaunchKernelGGL(ecfft_stage_kernel<C>, dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s, (XYZZ<F>*)a,
-                       (const uint4*)tw, log_n, st);
+                       (const uint4*)tw, log_n, st, (XYZZ<F>*)gt);
     ECG_HIP(hipGetLastError());
     ECG_TRY(kt_end(ctx, "ecfft_stage", s));
   }

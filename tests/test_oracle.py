@@ -172,3 +172,21 @@ def test_kat_construction(cid):
     for i in (0, 1, n - 1):
         pi = co.jac_to_affine(cid, co.gen_mul(cid, a + i * b))
         assert (pi == B[i]).all()
+
+
+def test_glv_constants():
+    """BLS12-381 G1 endomorphism used by the EC-FFT twiddle multiplications
+    (tools/gen_params.py GLV): LAMBDA^2 + LAMBDA + 1 = 0 mod r, BETA^3 = 1 in
+    Fq, and (BETA x, y) = LAMBDA * (x, y) for the generator and another point."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_params", os.path.join(os.path.dirname(GOLDEN), "..", "tools",
+                                                                          "gen_params.py"))
+    gp = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gp)
+    beta, lam = gp.GLV["bls12_381"]
+    c = po.BLS12_381
+    r, q = c.fr.modulus, c.fq.modulus
+    assert (lam * lam + lam + 1) % r == 0 and pow(beta, 3, q) == 1 and beta != 1
+    for k in (1, 0x1234567890ABCDEF):
+        P = po.jac_to_affine(po.scalar_mul((c.gx, c.gy), k, q), q)
+        assert (beta * P[0] % q, P[1]) == po.jac_to_affine(po.scalar_mul(P, lam, q), q)
