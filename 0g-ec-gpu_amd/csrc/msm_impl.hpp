@@ -39,6 +39,7 @@
 #pragma once
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -124,17 +125,16 @@ static MsmPlan make_plan(size_t n, uint32_t nbits, uint32_t forced_c = 0) {
 // ---------------------------------------------------------------------------
 // One thread per scalar j of the row; the digits are emitted once per line
 // (entry (w, line, j) -> key = group(line, chunk(j), w) * B + |d| - 1).
+// Scalar j reduced into s[0..7] (s[8] = 0 pads the window reads): optional
+// Montgomery -> canonical, then mod r.
 template <class C>
-__global__ void __launch_bounds__(MSM_THREADS)
-    msm_digits_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, uint32_t* __restrict__ keys,
-                      uint32_t* __restrict__ vals) {
-  const size_t m = (size_t)g.n_chunks * g.clen;
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
-  uint4 lo = scalars[2 * j], hi = scalars[2 * j + 1];
-  uint32_t s[9] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, 0};
+ECG_DEV void load_scalar(const uint4* __restrict__ scalars, size_t j, uint32_t mont, uint32_t* s) {
   using FrP = typename C::FrParams;
-  if (g.scalar_mont) {  // PrimeFieldRepr::to_bigint (ag-types/src/impls.rs:13) on device
+  const uint4 lo = scalars[2 * j], hi = scalars[2 * j + 1];
+  s[0] = lo.x; s[1] = lo.y; s[2] = lo.z; s[3] = lo.w;
+  s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
+  s[8] = 0;
+  if (mont) {  // PrimeFieldRepr::to_bigint (ag-types/src/impls.rs:13) on device
     Fp<FrP> m;
 #pragma unroll
     for (int k = 0; k < 8; k++) m.v[k] = s[k];
@@ -155,25 +155,44 @@ __global__ void __launch_bounds__(MSM_THREADS)
 #pragma unroll
     for (int k = 0; k < 8; k++) s[k] = t[k];
   }
-  const uint32_t chunk = g.n_chunks == 1 ? 0u : (uint32_t)(j / g.clen);
+}
+
+// Signed digit of window w (carry in/out), d in [-2^(c-1), 2^(c-1)].
+ECG_DEV int32_t window_digit(const uint32_t* s, uint32_t w, const MsmPlan& pl, uint32_t& carry) {
   const uint32_t mask = (1u << pl.c) - 1;
   const uint32_t half = 1u << (pl.c - 1);
+  const uint32_t bit = w * pl.c;
+  const uint32_t limb = bit >> 5, sh = bit & 31;
+  uint32_t v = 0;
+  if (limb < 8) {
+    const uint64_t two = (uint64_t)s[limb] | ((uint64_t)s[limb + 1] << 32);
+    v = (uint32_t)(two >> sh) & mask;
+  }
+  int32_t d = (int32_t)(v + carry);
+  carry = 0;
+  if (w + 1 < pl.W && (uint32_t)d >= half) {
+    d -= (int32_t)(1u << pl.c);
+    carry = 1;
+  }
+  return d;
+}
+
+// One thread per scalar j of the row; the digits are emitted once per line
+// (entry (w, line, j) -> key = group(line, chunk(j), w) * B + |d| - 1).
+template <class C>
+__global__ void __launch_bounds__(MSM_THREADS)
+    msm_digits_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, uint32_t* __restrict__ keys,
+                      uint32_t* __restrict__ vals) {
+  const size_t m = (size_t)g.n_chunks * g.clen;
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  uint32_t s[9];
+  load_scalar<C>(scalars, j, g.scalar_mont, s);
+  const uint32_t chunk = g.n_chunks == 1 ? 0u : (uint32_t)(j / g.clen);
   const uint32_t sentinel = pl.G * pl.B;
   uint32_t carry = 0;
   for (uint32_t w = 0; w < pl.W; w++) {
-    const uint32_t bit = w * pl.c;
-    const uint32_t limb = bit >> 5, sh = bit & 31;
-    uint32_t v = 0;
-    if (limb < 8) {
-      uint64_t two = (uint64_t)s[limb] | ((uint64_t)s[limb + 1] << 32);
-      v = (uint32_t)(two >> sh) & mask;
-    }
-    int32_t d = (int32_t)(v + carry);
-    carry = 0;
-    if (w + 1 < pl.W && (uint32_t)d >= half) {
-      d -= (int32_t)(1u << pl.c);
-      carry = 1;
-    }
+    const int32_t d = window_digit(s, w, pl, carry);
     const uint32_t mag = d < 0 ? (uint32_t)(-d) : (uint32_t)d;
     const uint32_t sign = d < 0 ? 0x80000000u : 0u;
     for (uint32_t l = 0; l < g.n_lines; l++) {
@@ -509,29 +528,34 @@ int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const M
   ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
   ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * pl.S / MSM_FOLD + pl.G) * sizeof(X), &pb));
 
+  // ---- group the (key, value) entries by bucket: rocPRIM onesweep radix sort
+  // (an MSD counting sort with 10-bit coarse bins was measured 3x slower:
+  // 13K bins leave ~0.15 entries per bin per tile, so its scatter cannot
+  // coalesce -- onesweep's 8-bit digits exist for exactly that reason)
+  const size_t ntot = total;
   hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(m, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
                      (const uint4*)d_scalars, g, pl, (uint32_t*)k0, (uint32_t*)v0);
   ECG_HIP(hipGetLastError());
-
   size_t tmp_bytes = 0;
   ECG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
                                              (uint32_t*)v1, total, 0, key_bits, s));
   ECG_TRY(ws_get(ctx, "msm_sort_tmp", tmp_bytes, &tmp));
   ECG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
                                              (uint32_t*)v1, total, 0, key_bits, s));
+  const size_t nseg_used = (ntot + pl.seg - 1) / pl.seg;
 
   // buckets nobody writes (no term) stay the identity: all-zero XYZZ (ZZ = 0)
   ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X), s));
 
   ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
-  hipLaunchKernelGGL(msm_accumulate_kernel<C>, dim3(blocks_for(nseg, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     (const F*)d_bases, (const uint32_t*)k1, (const uint32_t*)v1, total, sentinel, pl.seg, (X*)bk,
+  hipLaunchKernelGGL(msm_accumulate_kernel<C>, dim3(blocks_for(nseg_used, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                     (const F*)d_bases, (const uint32_t*)k1, (const uint32_t*)v1, ntot, sentinel, pl.seg, (X*)bk,
                      (X*)rc, (uint32_t*)rk);
   ECG_HIP(hipGetLastError());
   ECG_TRY(kt_end(ctx, "msm_accumulate", s));
 
   // combine the segment-edge partials, level by level
-  size_t nrec = 2 * nseg;
+  size_t nrec = 2 * nseg_used;
   X* rin = (X*)rc;
   uint32_t* kin = (uint32_t*)rk;
   X* rout = (X*)rc2;
