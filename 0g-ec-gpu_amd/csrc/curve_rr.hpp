@@ -1,0 +1,280 @@
+// XYZZ point arithmetic over the reduced-radix field (fieldrr.hpp) for the
+// MSM bucket pipeline: the same formulas as curve.hpp (madd-2008-s,
+// add-2008-s, dbl-2008-s-1 / mdbl-2008-s-1; ec.cl:17-130's role), with every
+// subtraction's multiple of p chosen from a value bound, so no value ever
+// needs a conditional reduction.  Bounds, in units of p (products M < 1.01 p
+// given the 2^25 slack):
+//   stored points  X <= 9.01, Y <= 5.01, ZZ, ZZZ <= M;   bases x, y <= M
+//   madd:  P = U2 - X1 + 32p <= 33, R = S2 - Y1 + 16p <= 17,
+//          X3 = R^2 - (PPP + 2Q) + 8p <= 9.01, D = Q - X3 + 32p <= 33,
+//          Y3 = R D - Y1 PPP + 4p <= 5.01
+//   add:   P, R <= 5.01 (+4p), the rest as madd
+//   dbl:   U = 2Y <= 10.02, M = 3X^2 <= 3.03, X3, Y3 as madd
+// Largest product of operand bounds: 17 x 33 = 561 << 2^24.
+// Exceptional cases (P = 0 mod p: doubling or inverse) are detected on PP =
+// P^2, a product output, whose low limb screens them behind a branch that
+// waves almost never take.  The identity is the all-zero ZZ marker.
+#pragma once
+#include "curve.hpp"
+#include "fieldrr.hpp"
+
+namespace ecg {
+
+template <class Q>
+ECG_DEV bool xyzz_is_zero_rr(const XYZZ<FpR<Q>>& p) {
+  return fis_zero(p.ZZ);
+}
+
+// mdbl-2008-s-1: 2 (x, y), x <= M, y <= 4p
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> rr_dbl_affine(const Affine<FpR<Q>>& a) {
+  using F = FpR<Q>;
+  const F U = rr_add(a.y, a.y);
+  const F V = rr_sqr(U);
+  const F W = rr_mul(U, V);
+  const F S = rr_mul(a.x, V);
+  const F X2 = rr_sqr(a.x);
+  const F Mm = rr_add(rr_add(X2, X2), X2);
+  XYZZ<F> r;
+  r.X = rr_sub<8>(rr_sqr(Mm), rr_add(S, S));
+  r.Y = rr_sub<4>(rr_mul(Mm, rr_sub<32>(S, r.X)), rr_mul(W, a.y));
+  r.ZZ = V;
+  r.ZZZ = W;
+  return r;
+}
+
+// dbl-2008-s-1: 2 P
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> rr_dbl(const XYZZ<FpR<Q>>& p) {
+  using F = FpR<Q>;
+  if (xyzz_is_zero_rr(p)) return p;
+  const F U = rr_add(p.Y, p.Y);
+  const F V = rr_sqr(U);
+  const F W = rr_mul(U, V);
+  const F S = rr_mul(p.X, V);
+  const F X2 = rr_sqr(p.X);
+  const F Mm = rr_add(rr_add(X2, X2), X2);
+  XYZZ<F> r;
+  r.X = rr_sub<8>(rr_sqr(Mm), rr_add(S, S));
+  r.Y = rr_sub<4>(rr_mul(Mm, rr_sub<32>(S, r.X)), rr_mul(W, p.Y));
+  r.ZZ = rr_mul(V, p.ZZ);
+  r.ZZZ = rr_mul(W, p.ZZZ);
+  return r;
+}
+
+// madd-2008-s: P + (x2, y2); `a` must not be the identity.  The ten
+// products run as five independent pairs (rr_mul2 / rr_sqr2).
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> rr_add_affine(const XYZZ<FpR<Q>>& p, const Affine<FpR<Q>>& a) {
+  using F = FpR<Q>;
+  if (xyzz_is_zero_rr(p)) {
+    XYZZ<F> r;
+    r.X = a.x;
+    r.Y = a.y;
+    r.ZZ = F::one();
+    r.ZZZ = F::one();
+    return r;
+  }
+  F U2, S2, PP, RR, PPP, Qv, T, Y3b;
+  rr_mul2(a.x, p.ZZ, a.y, p.ZZZ, U2, S2);
+  const F P = rr_sub<32>(U2, p.X);
+  const F R = rr_sub<16>(S2, p.Y);
+  rr_sqr2(P, R, PP, RR);
+  rr_mul2(P, PP, p.X, PP, PPP, Qv);
+  XYZZ<F> r;
+  rr_mul2(p.ZZ, PP, p.ZZZ, PPP, r.ZZ, r.ZZZ);
+  r.X = rr_sub<8>(RR, rr_add(rr_add(PPP, Qv), Qv));
+  rr_mul2(R, rr_sub<32>(Qv, r.X), p.Y, PPP, T, Y3b);
+  r.Y = rr_sub<4>(T, Y3b);
+  if (rr_maybe_zero_prod(PP)) {  // rare: P = Q or P = -Q
+    if (rr_is_zero_prod(PP)) {
+      if (rr_is_zero_prod(RR)) return rr_dbl_affine(a);
+      return xyzz_zero<F>();
+    }
+  }
+  return r;
+}
+
+// add-2008-s: P + Q (seven product pairs)
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> rr_add_xyzz(const XYZZ<FpR<Q>>& p, const XYZZ<FpR<Q>>& q) {
+  using F = FpR<Q>;
+  if (xyzz_is_zero_rr(p)) return q;
+  if (xyzz_is_zero_rr(q)) return p;
+  F U1, U2, S1, S2, PP, RR, PPP, Qv, ZZ12, ZZZ12, T, Y3b;
+  rr_mul2(p.X, q.ZZ, q.X, p.ZZ, U1, U2);
+  rr_mul2(p.Y, q.ZZZ, q.Y, p.ZZZ, S1, S2);
+  const F P = rr_sub<4>(U2, U1);
+  const F R = rr_sub<4>(S2, S1);
+  rr_sqr2(P, R, PP, RR);
+  rr_mul2(P, PP, U1, PP, PPP, Qv);
+  rr_mul2(p.ZZ, q.ZZ, p.ZZZ, q.ZZZ, ZZ12, ZZZ12);
+  XYZZ<F> r;
+  rr_mul2(ZZ12, PP, ZZZ12, PPP, r.ZZ, r.ZZZ);
+  r.X = rr_sub<8>(RR, rr_add(rr_add(PPP, Qv), Qv));
+  rr_mul2(R, rr_sub<32>(Qv, r.X), S1, PPP, T, Y3b);
+  r.Y = rr_sub<4>(T, Y3b);
+  if (rr_maybe_zero_prod(PP)) {
+    if (rr_is_zero_prod(PP)) {
+      if (rr_is_zero_prod(RR)) return rr_dbl(p);
+      return xyzz_zero<F>();
+    }
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// point-arithmetic policy used by the MSM kernels (msm_impl.hpp): one name per
+// operation, overloaded on the coordinate field -- the 32-bit-limb lazy
+// formulas of curve.hpp (G2 over Fq2, A/B) or the reduced-radix ones above.
+// ---------------------------------------------------------------------------
+template <class F>
+ECG_DEV XYZZ<F> pa_add_affine(const XYZZ<F>& p, const Affine<F>& a) {
+  return xyzz_add_affine<F, true>(p, a);
+}
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> pa_add_affine(const XYZZ<FpR<Q>>& p, const Affine<FpR<Q>>& a) {
+  return rr_add_affine(p, a);
+}
+
+template <class F>
+ECG_DEV XYZZ<F> pa_add(const XYZZ<F>& p, const XYZZ<F>& q) {
+  return xyzz_add<F, true>(p, q);
+}
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> pa_add(const XYZZ<FpR<Q>>& p, const XYZZ<FpR<Q>>& q) {
+  return rr_add_xyzz(p, q);
+}
+
+template <class F>
+ECG_DEV XYZZ<F> pa_dbl(const XYZZ<F>& p) {
+  return xyzz_dbl<F, true>(p);
+}
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> pa_dbl(const XYZZ<FpR<Q>>& p) {
+  return rr_dbl(p);
+}
+
+// negated base y (y <= M)
+template <class F>
+ECG_DEV F pa_neg_y(const F& y) {
+  return fneg_lz(y);
+}
+template <class Q>
+ECG_DEV FpR<Q> pa_neg_y(const FpR<Q>& y) {
+  return rr_neg<4>(y);
+}
+
+// k P for a small unsigned k (double-and-add from the MSB)
+template <class F>
+ECG_DEV XYZZ<F> pa_mul_small(const XYZZ<F>& p, uint32_t k) {
+  XYZZ<F> acc = xyzz_zero<F>();
+  if (k == 0) return acc;
+  const int top = 31 - __builtin_clz(k);
+  acc = p;
+  for (int b = top - 1; b >= 0; b--) {
+    acc = pa_dbl(acc);
+    if ((k >> b) & 1) acc = pa_add(acc, p);
+  }
+  return acc;
+}
+
+// bucket-pipeline point -> lazy 32-bit-limb XYZZ (canonical coordinates)
+template <class F>
+ECG_DEV XYZZ<F> pa_to_std(const XYZZ<F>& p) {
+  return p;
+}
+template <class Q>
+ECG_DEV XYZZ<Fp<typename Q::Base>> pa_to_std(const XYZZ<FpR<Q>>& p) {
+  XYZZ<Fp<typename Q::Base>> r;
+  if (xyzz_is_zero_rr(p)) return xyzz_zero<Fp<typename Q::Base>>();
+  r.X = rr_to_std(p.X);
+  r.Y = rr_to_std(p.Y);
+  r.ZZ = rr_to_std(p.ZZ);
+  r.ZZZ = rr_to_std(p.ZZZ);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// memory: a reduced-radix affine base is 2 NL words, an XYZZ point 4 NL words,
+// moved as 16-B vectors (NL even for both base-field layouts)
+// ---------------------------------------------------------------------------
+template <class Q, int W>
+ECG_DEV void rr_load_words(const void* src, uint32_t* w) {
+  static_assert(W % 4 == 0, "16-B vector moves");
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+  for (int i = 0; i < W / 4; i++) {
+    const uint4 t = s[i];
+    w[4 * i] = t.x;
+    w[4 * i + 1] = t.y;
+    w[4 * i + 2] = t.z;
+    w[4 * i + 3] = t.w;
+  }
+}
+
+template <class Q, int W>
+ECG_DEV void rr_store_words(void* dst, const uint32_t* w) {
+  static_assert(W % 4 == 0, "16-B vector moves");
+  uint4* d = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+  for (int i = 0; i < W / 4; i++) d[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+template <class Q>
+ECG_DEV Affine<FpR<Q>> load_affine(const FpR<Q>* xy) {
+  constexpr int NL = Q::NL;
+  uint32_t w[2 * NL];
+  rr_load_words<Q, 2 * NL>(xy, w);
+  Affine<FpR<Q>> a;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    a.x.v[i] = w[i];
+    a.y.v[i] = w[NL + i];
+  }
+  return a;
+}
+
+template <class Q>
+ECG_DEV void store_affine(FpR<Q>* xy, const Affine<FpR<Q>>& a) {
+  constexpr int NL = Q::NL;
+  uint32_t w[2 * NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    w[i] = a.x.v[i];
+    w[NL + i] = a.y.v[i];
+  }
+  rr_store_words<Q, 2 * NL>(xy, w);
+}
+
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> load_xyzz(const XYZZ<FpR<Q>>* src) {
+  constexpr int NL = Q::NL;
+  uint32_t w[4 * NL];
+  rr_load_words<Q, 4 * NL>(src, w);
+  XYZZ<FpR<Q>> p;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    p.X.v[i] = w[i];
+    p.Y.v[i] = w[NL + i];
+    p.ZZ.v[i] = w[2 * NL + i];
+    p.ZZZ.v[i] = w[3 * NL + i];
+  }
+  return p;
+}
+
+template <class Q>
+ECG_DEV void store_xyzz(XYZZ<FpR<Q>>* dst, const XYZZ<FpR<Q>>& p) {
+  constexpr int NL = Q::NL;
+  uint32_t w[4 * NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    w[i] = p.X.v[i];
+    w[NL + i] = p.Y.v[i];
+    w[2 * NL + i] = p.ZZ.v[i];
+    w[3 * NL + i] = p.ZZZ.v[i];
+  }
+  rr_store_words<Q, 4 * NL>(dst, w);
+}
+
+}  // namespace ecg

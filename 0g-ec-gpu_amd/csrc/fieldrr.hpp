@@ -1,0 +1,416 @@
+// Reduced-radix Montgomery arithmetic for the MSM bucket pipeline (gfx950).
+//
+// field.hpp's 32-bit-limb product needs a v_addc_co_u32 after every
+// v_mad_u64_u32 to catch the 64-bit accumulator's carry, and on gfx950 that
+// addc issues at the same cost as the mad itself (tools/issue_bench.hip:
+// mad, addc, add_co, mul_lo, alignbit all ~4 SIMD cycles per wave64; only
+// v_add_u32 is cheaper).  Here an element is NL limbs of BITS <= 29 bits:
+// every product is < 2^58, a whole column of 2*NL products fits a plain
+// 64-bit accumulator, and a product is ONE v_mad_u64_u32.  One shift per
+// column replaces the 2*L^2 carry instructions: the BLS12-381 Fq product
+// drops from ~640 to ~470 VALU instructions.
+//
+// Representation  FpR<Q>: value = sum v[i] 2^(BITS i) = x R' (mod p), with
+// R' = 2^(NL BITS) (Q = params::*_rr, tools/gen_params_rr.py).  The boundary
+// keeps ark-ff's R = 2^(64N) form; rr_from_std / rr_to_std convert (one
+// product each).  Values are redundant ("lazy"):
+//   * quasi-normalised (QN): limbs i < NL-1 below 2^BITS + 8, top limb holds
+//     the rest of the value;
+//   * rr_mul / rr_sqr: QN inputs of values a, b with a*b <= 2^SLACK_LOG2 p^2 / 2
+//     -> output (ab + mp)/R' < p + p/2, with EXACT limbs (< 2^BITS), so the
+//     output is the unique radix-2^BITS digit string of its value;
+//   * rr_add: exact sum, QN;  rr_sub<k>: a - b + k p, QN, for b <= k p / 2;
+//   * congruence to 0 of a product output v (< 2p) is  v == 0 || v == p.
+// The MSM formulas (curve_rr.hpp) keep every value below 64 p, far inside
+// the 2^25 (BLS12-381 Fq) / 2^26 (BN254 Fq) slack.  Outputs are converted back
+// and fully reduced, so results stay bit-identical to the reference's.
+#pragma once
+#include "field.hpp"
+
+namespace ecg {
+
+namespace params {
+#include "params_rr.inc"
+}
+
+template <class Q>
+struct FpR {
+  using Params = Q;
+  static constexpr int NL = Q::NL;
+  static constexpr int B = Q::BITS;
+  static constexpr uint32_t MASK = (1u << B) - 1;
+  uint32_t v[NL];
+
+  ECG_DEV static FpR zero() {
+    FpR r;
+#pragma unroll
+    for (int i = 0; i < NL; i++) r.v[i] = 0;
+    return r;
+  }
+  ECG_DEV static FpR one() {
+    FpR r;
+#pragma unroll
+    for (int i = 0; i < NL; i++) r.v[i] = Q::ONE[i];
+    return r;
+  }
+};
+
+// acc += a * b as ONE v_mad_u64_u32 (carry-out unused: the column sum never
+// exceeds 2^63).  Written as asm so that hipcc keeps one accumulator chain per
+// column instead of re-associating it into two chains joined by a 64-bit add
+// (measured: that costs ~8% more instructions per product).
+ECG_DEV void mad64(uint64_t& acc, uint32_t a, uint32_t b) {
+#if defined(ECG_RR_CXX_MAD)
+  acc += (uint64_t)a * b;
+#elif defined(ECG_RR_BAR_MAD)
+  acc += (uint64_t)a * b;
+  asm("" : "+v"(acc));
+#else
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
+#endif
+}
+ECG_DEV void mad64s(uint64_t& acc, uint32_t a, uint32_t b_uniform) {
+#if defined(ECG_RR_CXX_MAD)
+  acc += (uint64_t)a * b_uniform;
+#elif defined(ECG_RR_BAR_MAD)
+  acc += (uint64_t)a * b_uniform;
+  asm("" : "+v"(acc));
+#else
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "s"(b_uniform));
+#endif
+}
+
+// Montgomery product (a b + m p) / R', product scanning, one v_mad_u64_u32
+// per product.
+template <class Q>
+ECG_DEV FpR<Q> rr_mul(const FpR<Q>& a, const FpR<Q>& b) {
+  constexpr int NL = Q::NL, B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  uint32_t m[NL];
+  FpR<Q> r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int i = 0; i <= k; i++) mad64(acc, a.v[i], b.v[k - i]);
+#pragma unroll
+    for (int i = 0; i < k; i++) mad64s(acc, m[i], Q::P[k - i]);
+    m[k] = ((uint32_t)acc * Q::INV) & MASK;
+    mad64s(acc, m[k], Q::P[0]);  // low BITS bits of acc become 0
+    acc >>= B;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; i++) mad64(acc, a.v[i], b.v[k - i]);
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; i++) mad64s(acc, m[i], Q::P[k - i]);
+    r.v[k - NL] = (uint32_t)acc & MASK;
+    acc >>= B;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+// Two independent products column by column, their mads paired in one asm
+// statement: two dependency chains in flight per wave (latency cover at 2
+// waves/SIMD) and one hazard s_nop per pair instead of per product.
+ECG_DEV void mad64x2(uint64_t& acc0, uint32_t a0, uint32_t b0, uint64_t& acc1, uint32_t a1, uint32_t b1) {
+  uint64_t c0, c1;
+  asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %6, %7, %1"
+      : "+v"(acc0), "+v"(acc1), "=&s"(c0), "=&s"(c1)
+      : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+}
+ECG_DEV void mad64x2s(uint64_t& acc0, uint32_t a0, uint64_t& acc1, uint32_t a1, uint32_t b_uniform) {
+  uint64_t c0, c1;
+  asm("v_mad_u64_u32 %0, %2, %4, %6, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %5, %6, %1"
+      : "+v"(acc0), "+v"(acc1), "=&s"(c0), "=&s"(c1)
+      : "v"(a0), "v"(a1), "s"(b_uniform));
+}
+
+// r0 = a0 b0 / R', r1 = a1 b1 / R'
+template <class Q>
+ECG_DEV void rr_mul2(const FpR<Q>& a0, const FpR<Q>& b0, const FpR<Q>& a1, const FpR<Q>& b1, FpR<Q>& r0,
+                     FpR<Q>& r1) {
+  constexpr int NL = Q::NL, B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  uint32_t m0[NL], m1[NL];
+  uint64_t x0 = 0, x1 = 0;
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+#pragma unroll
+    for (int i = 0; i <= k; i++) mad64x2(x0, a0.v[i], b0.v[k - i], x1, a1.v[i], b1.v[k - i]);
+#pragma unroll
+    for (int i = 0; i < k; i++) mad64x2s(x0, m0[i], x1, m1[i], Q::P[k - i]);
+    m0[k] = ((uint32_t)x0 * Q::INV) & MASK;
+    m1[k] = ((uint32_t)x1 * Q::INV) & MASK;
+    mad64x2s(x0, m0[k], x1, m1[k], Q::P[0]);
+    x0 >>= B;
+    x1 >>= B;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; k++) {
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; i++) mad64x2(x0, a0.v[i], b0.v[k - i], x1, a1.v[i], b1.v[k - i]);
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; i++) mad64x2s(x0, m0[i], x1, m1[i], Q::P[k - i]);
+    r0.v[k - NL] = (uint32_t)x0 & MASK;
+    r1.v[k - NL] = (uint32_t)x1 & MASK;
+    x0 >>= B;
+    x1 >>= B;
+  }
+  r0.v[NL - 1] = (uint32_t)x0;
+  r1.v[NL - 1] = (uint32_t)x1;
+}
+
+// r0 = a0^2 / R', r1 = a1^2 / R'
+template <class Q>
+ECG_DEV void rr_sqr2(const FpR<Q>& a0, const FpR<Q>& a1, FpR<Q>& r0, FpR<Q>& r1) {
+  constexpr int NL = Q::NL, B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  uint32_t m0[NL], m1[NL], d0[NL], d1[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    d0[i] = a0.v[i] + a0.v[i];
+    d1[i] = a1.v[i] + a1.v[i];
+  }
+  uint64_t x0 = 0, x1 = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * NL - 1; k++) {
+    const int i0 = k < NL ? 0 : k - NL + 1;
+#pragma unroll
+    for (int i = i0; 2 * i < k; i++) mad64x2(x0, d0[i], a0.v[k - i], x1, d1[i], a1.v[k - i]);
+    if ((k & 1) == 0) mad64x2(x0, a0.v[k >> 1], a0.v[k >> 1], x1, a1.v[k >> 1], a1.v[k >> 1]);
+    if (k < NL) {
+#pragma unroll
+      for (int i = 0; i < k; i++) mad64x2s(x0, m0[i], x1, m1[i], Q::P[k - i]);
+      m0[k] = ((uint32_t)x0 * Q::INV) & MASK;
+      m1[k] = ((uint32_t)x1 * Q::INV) & MASK;
+      mad64x2s(x0, m0[k], x1, m1[k], Q::P[0]);
+    } else {
+#pragma unroll
+      for (int i = k - NL + 1; i < NL; i++) mad64x2s(x0, m0[i], x1, m1[i], Q::P[k - i]);
+      r0.v[k - NL] = (uint32_t)x0 & MASK;
+      r1.v[k - NL] = (uint32_t)x1 & MASK;
+    }
+    x0 >>= B;
+    x1 >>= B;
+  }
+  r0.v[NL - 1] = (uint32_t)x0;
+  r1.v[NL - 1] = (uint32_t)x1;
+}
+
+// Squaring: off-diagonal products once, against a doubled operand (2 a_i <
+// 2^(BITS+1) + 16 keeps every product < 2^59): ~NL^2/2 fewer products.
+template <class Q>
+ECG_DEV FpR<Q> rr_sqr(const FpR<Q>& a) {
+  constexpr int NL = Q::NL, B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  uint32_t m[NL], a2[NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) a2[i] = a.v[i] + a.v[i];
+  FpR<Q> r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * NL - 1; k++) {
+    const int i0 = k < NL ? 0 : k - NL + 1;
+#pragma unroll
+    for (int i = i0; 2 * i < k; i++) mad64(acc, a2[i], a.v[k - i]);
+    if ((k & 1) == 0) mad64(acc, a.v[k >> 1], a.v[k >> 1]);
+    if (k < NL) {
+#pragma unroll
+      for (int i = 0; i < k; i++) mad64s(acc, m[i], Q::P[k - i]);
+      m[k] = ((uint32_t)acc * Q::INV) & MASK;
+      mad64s(acc, m[k], Q::P[0]);
+    } else {
+#pragma unroll
+      for (int i = k - NL + 1; i < NL; i++) mad64s(acc, m[i], Q::P[k - i]);
+      r.v[k - NL] = (uint32_t)acc & MASK;
+    }
+    acc >>= B;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+  return r;
+}
+
+// One parallel carry step: limb i keeps its low BITS bits plus the carry of
+// limb i-1 (s[i] < 2^32 on entry -> QN on exit); the top limb keeps all bits.
+template <class Q>
+ECG_DEV FpR<Q> rr_carry(const uint32_t* s) {
+  constexpr int NL = Q::NL, B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  FpR<Q> r;
+  r.v[0] = s[0] & MASK;
+#pragma unroll
+  for (int i = 1; i < NL - 1; i++) r.v[i] = (s[i] & MASK) + (s[i - 1] >> B);
+  r.v[NL - 1] = s[NL - 1] + (s[NL - 2] >> B);
+  return r;
+}
+
+template <class Q>
+ECG_DEV FpR<Q> rr_add(const FpR<Q>& a, const FpR<Q>& b) {
+  uint32_t s[Q::NL];
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) s[i] = a.v[i] + b.v[i];
+  return rr_carry<Q>(s);
+}
+
+template <int K>
+constexpr int kp_index() {
+  static_assert(K >= 2 && (K & (K - 1)) == 0 && K <= 64, "k must be a power of two in [2, 64]");
+  return K == 2 ? 0 : K == 4 ? 1 : K == 8 ? 2 : K == 16 ? 3 : K == 32 ? 4 : 5;
+}
+
+// a - b + K p  (requires value(b) <= K p / 2)
+template <int K, class Q>
+ECG_DEV FpR<Q> rr_sub(const FpR<Q>& a, const FpR<Q>& b) {
+  constexpr int j = kp_index<K>();
+  static_assert((Q::KP_OK >> j) & 1, "K p not representable for this field (tools/gen_params_rr.py)");
+  uint32_t s[Q::NL];
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) s[i] = a.v[i] + Q::KP[j][i] - b.v[i];
+  return rr_carry<Q>(s);
+}
+
+// K p - a  (requires value(a) <= K p / 2)
+template <int K, class Q>
+ECG_DEV FpR<Q> rr_neg(const FpR<Q>& a) {
+  constexpr int j = kp_index<K>();
+  static_assert((Q::KP_OK >> j) & 1, "K p not representable for this field (tools/gen_params_rr.py)");
+  uint32_t s[Q::NL];
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) s[i] = Q::KP[j][i] - a.v[i];
+  return rr_carry<Q>(s);
+}
+
+// exact all-zero limbs (the identity marker; never a product output of a
+// non-zero value)
+template <class Q>
+ECG_DEV bool fis_zero(const FpR<Q>& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) o |= a.v[i];
+  return o == 0;
+}
+
+// v == 0 (mod p) for a product output (exact limbs, value < 2p)
+template <class Q>
+ECG_DEV bool rr_is_zero_prod(const FpR<Q>& a) {
+  uint32_t o = 0, q = 0;
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) {
+    o |= a.v[i];
+    q |= a.v[i] ^ Q::P[i];
+  }
+  return o == 0 || q == 0;
+}
+
+// cheap necessary condition for rr_is_zero_prod (low limb only): lets the
+// rare exceptional paths sit behind a wave-uniform branch
+template <class Q>
+ECG_DEV bool rr_maybe_zero_prod(const FpR<Q>& a) {
+  return a.v[0] == 0 || a.v[0] == Q::P[0];
+}
+
+// ---------------------------------------------------------------------------
+// radix change: 32-bit words <-> BITS-bit limbs (exact integers)
+// ---------------------------------------------------------------------------
+template <class Q, int L>
+ECG_DEV void rr_unpack(const uint32_t* w, uint32_t* limb) {
+  constexpr int B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) {
+    const int bit = B * i, j = bit >> 5, s = bit & 31;
+    uint32_t v = j < L ? w[j] >> s : 0u;
+    if (s != 0 && 32 - s < B && j + 1 < L) v |= w[j + 1] << (32 - s);
+    limb[i] = v & MASK;
+  }
+}
+
+template <class Q, int L>
+ECG_DEV void rr_pack(const uint32_t* limb, uint32_t* w) {
+  constexpr int B = Q::BITS;
+#pragma unroll
+  for (int j = 0; j < L; j++) {
+    const int bit = 32 * j, i = bit / B, s = bit % B;
+    uint32_t v = i < Q::NL ? limb[i] >> s : 0u;
+    if (B - s < 32 && i + 1 < Q::NL) v |= limb[i + 1] << (B - s);
+    if (2 * B - s < 32 && i + 2 < Q::NL) v |= limb[i + 2] << (2 * B - s);
+    w[j] = v;
+  }
+}
+
+// ark-ff Montgomery (x R, 32-bit limbs, < p) -> x R' (product output form)
+template <class Q>
+ECG_DEV FpR<Q> rr_from_std(const Fp<typename Q::Base>& a) {
+  FpR<Q> x, c;
+  rr_unpack<Q, Fp<typename Q::Base>::L>(a.v, x.v);
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) c.v[i] = Q::TO_RR[i];
+  return rr_mul(x, c);
+}
+
+// x R' (any lazy value <= 64 p) -> canonical ark-ff Montgomery x R (< p)
+template <class Q>
+ECG_DEV Fp<typename Q::Base> rr_to_std(const FpR<Q>& a) {
+  constexpr int NL = Q::NL, B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  FpR<Q> c;
+#pragma unroll
+  for (int i = 0; i < NL; i++) c.v[i] = Q::FROM_RR[i];
+  FpR<Q> y = rr_mul(a, c);  // x R, exact limbs, value < 2p
+  uint32_t t[NL];
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {  // t = y - p, sequential borrow
+    const int32_t d = (int32_t)y.v[i] - (int32_t)Q::P[i] + br;
+    t[i] = (uint32_t)d & MASK;
+    br = d >> B;  // 0 or -1
+  }
+  const bool ge = br == 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) y.v[i] = ge ? t[i] : y.v[i];
+  Fp<typename Q::Base> r;
+  rr_pack<Q, Fp<typename Q::Base>::L>(y.v, r.v);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// memory: NL words, moved as 16-B vectors where NL allows
+// ---------------------------------------------------------------------------
+template <class Q>
+ECG_DEV FpR<Q> load(const FpR<Q>* p) {
+  FpR<Q> r;
+  if constexpr (Q::NL % 2 == 0) {
+    const uint2* s = reinterpret_cast<const uint2*>(p);
+#pragma unroll
+    for (int i = 0; i < Q::NL / 2; i++) {
+      const uint2 t = s[i];
+      r.v[2 * i] = t.x;
+      r.v[2 * i + 1] = t.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < Q::NL; i++) r.v[i] = p->v[i];
+  }
+  return r;
+}
+
+template <class Q>
+ECG_DEV void store(FpR<Q>* p, const FpR<Q>& a) {
+  if constexpr (Q::NL % 2 == 0) {
+    uint2* d = reinterpret_cast<uint2*>(p);
+#pragma unroll
+    for (int i = 0; i < Q::NL / 2; i++) d[i] = make_uint2(a.v[2 * i], a.v[2 * i + 1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < Q::NL; i++) p->v[i] = a.v[i];
+  }
+}
+
+}  // namespace ecg

@@ -46,6 +46,7 @@
 
 #include "ctx.hpp"
 #include "curve.hpp"
+#include "curve_rr.hpp"
 #include "dispatch.hpp"
 #include "host_field.hpp"
 
@@ -230,13 +231,11 @@ constexpr uint32_t KEY_END = 0xffffffffu;
 #define ECG_ACC_ATTR
 #endif
 
-template <class C>
+template <class F>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
-    msm_accumulate_kernel(const typename C::Fq* __restrict__ bases, const uint32_t* __restrict__ keys,
+    msm_accumulate_kernel(const F* __restrict__ bases, const uint32_t* __restrict__ keys,
                           const uint32_t* __restrict__ vals, size_t total, uint32_t sentinel, uint32_t seg,
-                          XYZZ<typename C::Fq>* __restrict__ buckets, XYZZ<typename C::Fq>* __restrict__ recs,
-                          uint32_t* __restrict__ rkeys) {
-  using F = typename C::Fq;
+                          XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ recs, uint32_t* __restrict__ rkeys) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t e0 = t * seg;
   if (e0 >= total) return;
@@ -262,9 +261,9 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
     Affine<F> Pn;
     if (kn < sentinel) Pn = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
     if (!aff_is_identity(P)) {  // GpuRepr identity (impls.rs:52-54) contributes nothing
-      F ny = fneg_lz(P.y);  // 2p - y: one subtraction (lazy range)
+      F ny = pa_neg_y(P.y);  // k p - y: one subtraction (lazy range)
       if (v >> 31) P.y = ny;
-      acc = xyzz_add_affine<F, true>(acc, P);
+      acc = pa_add_affine(acc, P);
     }
     if (kn != b) {
       const bool last = kn >= sentinel;  // end of segment or of the non-zero digits
@@ -301,12 +300,11 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
 //    O(log) levels, not a serial walk.  The last level (one segment) stores
 //    every run.  Buckets never written stay at the memset identity (ZZ = 0).
 // ---------------------------------------------------------------------------
-template <class C>
+template <class F>
 __global__ void __launch_bounds__(MSM_THREADS)
-    msm_combine_kernel(const XYZZ<typename C::Fq>* __restrict__ rin, const uint32_t* __restrict__ kin, size_t n,
-                       uint32_t sentinel, uint32_t seg, int final_level, XYZZ<typename C::Fq>* __restrict__ buckets,
-                       XYZZ<typename C::Fq>* __restrict__ rout, uint32_t* __restrict__ kout) {
-  using F = typename C::Fq;
+    msm_combine_kernel(const XYZZ<F>* __restrict__ rin, const uint32_t* __restrict__ kin, size_t n,
+                       uint32_t sentinel, uint32_t seg, int final_level, XYZZ<F>* __restrict__ buckets,
+                       XYZZ<F>* __restrict__ rout, uint32_t* __restrict__ kout) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t e0 = t * seg;
   if (e0 >= n) return;
@@ -326,7 +324,7 @@ __global__ void __launch_bounds__(MSM_THREADS)
   bool first_run = true;
   for (size_t e = e0; e < e1; e++) {
     const uint32_t kn = e + 1 < e1 ? kin[e + 1] : KEY_END;
-    acc = xyzz_add<F, true>(acc, load_xyzz(&rin[e]));
+    acc = pa_add(acc, load_xyzz(&rin[e]));
     if (kn != b) {
       const bool last = kn >= sentinel;
       if (final_level) {
@@ -357,40 +355,89 @@ __global__ void __launch_bounds__(MSM_THREADS)
 // ---------------------------------------------------------------------------
 // 5. per-segment summation by parts
 // ---------------------------------------------------------------------------
-template <class C>
+template <class F>
 __global__ void __launch_bounds__(MSM_THREADS)
-    msm_reduce_kernel(const XYZZ<typename C::Fq>* __restrict__ buckets, MsmPlan pl,
-                      XYZZ<typename C::Fq>* __restrict__ partial) {
-  using F = typename C::Fq;
+    msm_reduce_kernel(const XYZZ<F>* __restrict__ buckets, MsmPlan pl, XYZZ<F>* __restrict__ partial) {
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= pl.G * pl.S) return;
   const uint32_t w = id / pl.S, sgm = id % pl.S;
   const XYZZ<F>* bk = buckets + (size_t)w * pl.B + (size_t)sgm * pl.LS;
   XYZZ<F> run = xyzz_zero<F>(), acc = xyzz_zero<F>();
   for (int j = (int)pl.LS - 1; j >= 0; j--) {
-    run = xyzz_add<F, true>(run, load_xyzz(&bk[j]));
-    acc = xyzz_add<F, true>(acc, run);
+    run = pa_add(run, load_xyzz(&bk[j]));
+    acc = pa_add(acc, run);
   }
   // acc = sum_j (j+1) S_j ; add (sgm*LS) * run for the segment offset
-  if (sgm != 0) acc = xyzz_add<F, true>(acc, xyzz_mul_small<F, true>(run, sgm * pl.LS));
+  if (sgm != 0) acc = pa_add(acc, pa_mul_small(run, sgm * pl.LS));
   store_xyzz(&partial[id], acc);
 }
 
 // ---------------------------------------------------------------------------
 // 6. fold `cnt` consecutive points per group into ceil(cnt / MSM_FOLD)
 // ---------------------------------------------------------------------------
-template <class C>
+template <class F>
 __global__ void __launch_bounds__(MSM_THREADS)
-    msm_sum_kernel(const XYZZ<typename C::Fq>* __restrict__ in, uint32_t W, uint32_t cnt, uint32_t out_cnt,
-                   XYZZ<typename C::Fq>* __restrict__ out) {
-  using F = typename C::Fq;
+    msm_sum_kernel(const XYZZ<F>* __restrict__ in, uint32_t W, uint32_t cnt, uint32_t out_cnt,
+                   XYZZ<F>* __restrict__ out) {
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= W * out_cnt) return;
   const uint32_t w = id / out_cnt, o = id % out_cnt;
   const uint32_t j0 = o * MSM_FOLD, j1 = min(j0 + MSM_FOLD, cnt);
   XYZZ<F> acc = xyzz_zero<F>();
-  for (uint32_t j = j0; j < j1; j++) acc = xyzz_add<F, true>(acc, load_xyzz(&in[(size_t)w * cnt + j]));
+  for (uint32_t j = j0; j < j1; j++) acc = pa_add(acc, load_xyzz(&in[(size_t)w * cnt + j]));
   store_xyzz(&out[id], acc);
+}
+
+// ---------------------------------------------------------------------------
+// reduced-radix pipeline (curve_rr.hpp): bases into the R' form before step 3,
+// window sums back to the 32-bit-limb form after step 6
+// ---------------------------------------------------------------------------
+template <class Q>
+__global__ void __launch_bounds__(MSM_THREADS)
+    msm_rr_bases_kernel(const Fp<typename Q::Base>* __restrict__ in, size_t n, FpR<Q>* __restrict__ out) {
+  using F = Fp<typename Q::Base>;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Affine<F> a = load_affine(in + 2 * i);
+  Affine<FpR<Q>> r;
+  if (aff_is_identity(a)) {  // GpuRepr identity stays all-zero (impls.rs:52-54)
+    r.x = FpR<Q>::zero();
+    r.y = FpR<Q>::zero();
+  } else {
+    r.x = rr_from_std<Q>(a.x);
+    r.y = rr_from_std<Q>(a.y);
+  }
+  store_affine(out + 2 * i, r);
+}
+
+template <class F, class FS>
+__global__ void msm_sums_to_std_kernel(const XYZZ<F>* __restrict__ in, uint32_t n, XYZZ<FS>* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  store_xyzz(&out[i], pa_to_std(load_xyzz(&in[i])));
+}
+
+// Coordinate field of the bucket pipeline: the reduced-radix form for the G1
+// base fields, the 32-bit-limb lazy form for G2 (Fq2).
+template <class FqP>
+struct RRof {
+  using Q = void;
+};
+template <>
+struct RRof<params::bls12_381_fq> {
+  using Q = params::bls12_381_fq_rr;
+};
+template <>
+struct RRof<params::bn254_fq> {
+  using Q = params::bn254_fq_rr;
+};
+template <class C>
+constexpr bool msm_has_rr() {
+  return C::EXT == 1 && !std::is_same<typename RRof<typename C::FqParams>::Q, void>::value;
+}
+static bool msm_rr_enabled() {  // A/B switch: ECG_MSM_RR=0 runs the 32-bit-limb pipeline
+  static const bool v = env_u32("ECG_MSM_RR", 1) != 0;
+  return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -501,10 +548,12 @@ static inline uint32_t blocks_for(size_t n, int threads) { return (uint32_t)((n 
 
 // Steps 1-6 for one device pass: leaves pl.G window sums (lazy XYZZ) on the
 // device and returns their address in *d_sums.
-template <class C>
-int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
-                      const MsmPlan& pl, hipStream_t s, void** d_sums) {
-  using F = typename C::Fq;
+// AF = coordinate field of the bucket pipeline (C::Fq, or FpR<Q> for the
+// reduced-radix form, whose bases are converted first).
+template <class C, class AF>
+int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
+                  const MsmPlan& pl, hipStream_t s, void** d_sums) {
+  using F = AF;
   using X = XYZZ<F>;
   const size_t m = (size_t)g.n_chunks * g.clen;  // scalars consumed
   const size_t total = (size_t)pl.W * g.n_lines * m;
@@ -547,9 +596,20 @@ int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const M
   // buckets nobody writes (no term) stay the identity: all-zero XYZZ (ZZ = 0)
   ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X), s));
 
+  const F* bases = (const F*)d_bases;
+  if constexpr (!std::is_same<F, typename C::Fq>::value) {
+    const size_t nb_in = (size_t)g.n_lines * g.line_len;  // every base a value can index
+    void* rb;
+    ECG_TRY(ws_get(ctx, "msm_rr_bases", nb_in * 2 * sizeof(F), &rb));
+    hipLaunchKernelGGL(msm_rr_bases_kernel<typename F::Params>, dim3(blocks_for(nb_in, MSM_THREADS)),
+                       dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, nb_in, (F*)rb);
+    ECG_HIP(hipGetLastError());
+    bases = (const F*)rb;
+  }
+
   ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
-  hipLaunchKernelGGL(msm_accumulate_kernel<C>, dim3(blocks_for(nseg_used, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     (const F*)d_bases, (const uint32_t*)k1, (const uint32_t*)v1, ntot, sentinel, pl.seg, (X*)bk,
+  hipLaunchKernelGGL(msm_accumulate_kernel<F>, dim3(blocks_for(nseg_used, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                     bases, (const uint32_t*)k1, (const uint32_t*)v1, ntot, sentinel, pl.seg, (X*)bk,
                      (X*)rc, (uint32_t*)rk);
   ECG_HIP(hipGetLastError());
   ECG_TRY(kt_end(ctx, "msm_accumulate", s));
@@ -563,7 +623,7 @@ int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const M
   for (;;) {
     const bool fin = nrec <= MSM_COMBINE_SEG;
     const size_t nthr = (nrec + MSM_COMBINE_SEG - 1) / MSM_COMBINE_SEG;
-    hipLaunchKernelGGL(msm_combine_kernel<C>, dim3(blocks_for(nthr, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+    hipLaunchKernelGGL(msm_combine_kernel<F>, dim3(blocks_for(nthr, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
                        (const X*)rin, (const uint32_t*)kin, nrec, sentinel, MSM_COMBINE_SEG, fin ? 1 : 0, (X*)bk,
                        rout, kout);
     ECG_HIP(hipGetLastError());
@@ -573,7 +633,7 @@ int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const M
     std::swap(kin, kout);
   }
 
-  hipLaunchKernelGGL(msm_reduce_kernel<C>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
+  hipLaunchKernelGGL(msm_reduce_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
                      dim3(MSM_THREADS), 0, s, (const X*)bk, pl, (X*)pa);
   ECG_HIP(hipGetLastError());
 
@@ -582,7 +642,7 @@ int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const M
   X* out = (X*)pb;
   while (cnt > 1) {
     const uint32_t oc = (cnt + MSM_FOLD - 1) / MSM_FOLD;
-    hipLaunchKernelGGL(msm_sum_kernel<C>, dim3(blocks_for((size_t)pl.G * oc, MSM_THREADS)), dim3(MSM_THREADS),
+    hipLaunchKernelGGL(msm_sum_kernel<F>, dim3(blocks_for((size_t)pl.G * oc, MSM_THREADS)), dim3(MSM_THREADS),
                        0, s, (const X*)in, pl.G, cnt, oc, out);
     ECG_HIP(hipGetLastError());
     X* t = in;
@@ -590,8 +650,29 @@ int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const M
     out = t;
     cnt = oc;
   }
-  *d_sums = in;
+  if constexpr (std::is_same<F, typename C::Fq>::value) {
+    *d_sums = in;
+  } else {  // window sums back to the 32-bit-limb form (canonical coordinates)
+    void* st;
+    ECG_TRY(ws_get(ctx, "msm_sums_std", (size_t)pl.G * sizeof(XYZZ<typename C::Fq>), &st));
+    hipLaunchKernelGGL((msm_sums_to_std_kernel<F, typename C::Fq>), dim3(blocks_for(pl.G, 64)), dim3(64), 0, s,
+                       (const X*)in, pl.G, (XYZZ<typename C::Fq>*)st);
+    ECG_HIP(hipGetLastError());
+    *d_sums = st;
+  }
   return ECG_OK;
+}
+
+// Steps 1-6; leaves pl.G window sums (lazy 32-bit-limb XYZZ) on the device.
+template <class C>
+int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g, const MsmPlan& pl,
+               hipStream_t s, void** d_sums) {
+  if constexpr (msm_has_rr<C>()) {
+    if (msm_rr_enabled())
+      return msm_core_impl<C, FpR<typename RRof<typename C::FqParams>::Q>>(ctx, d_bases, d_scalars, g, pl, s,
+                                                                            d_sums);
+  }
+  return msm_core_impl<C, typename C::Fq>(ctx, d_bases, d_scalars, g, pl, s, d_sums);
 }
 
 // One MSM, processed in device passes of at most MSM_MAX_CHUNK terms; the
