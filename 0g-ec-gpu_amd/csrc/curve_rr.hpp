@@ -2,15 +2,17 @@
 // MSM bucket pipeline: the same formulas as curve.hpp (madd-2008-s,
 // add-2008-s, dbl-2008-s-1 / mdbl-2008-s-1; ec.cl:17-130's role), with every
 // subtraction's multiple of p chosen from a value bound, so no value ever
-// needs a conditional reduction.  Bounds, in units of p (products M < 1.01 p
-// given the 2^25 slack):
-//   stored points  X <= 9.01, Y <= 5.01, ZZ, ZZZ <= M;   bases x, y <= M
-//   madd:  P = U2 - X1 + 32p <= 33, R = S2 - Y1 + 16p <= 17,
-//          X3 = R^2 - (PPP + 2Q) + 8p <= 9.01, D = Q - X3 + 32p <= 33,
-//          Y3 = R D - Y1 PPP + 4p <= 5.01
+// needs a conditional reduction.  Bounds, in units of p (product outputs
+// M < 1.01 p given the >= 2^25 slack):
+//   stored points  X <= 17.01, Y <= 4.01, ZZ, ZZZ <= M;  bases x, y <= M,
+//                  a negated base y is 4p - y (<= 4p, "wide" limbs)
+//   madd:  P = U2 - X1 + 64p <= 65, R = S2 - Y1 + 16p <= 17,
+//          X3 = R^2 - PPP - 2Q + 16p <= 17.01, D = Q - X3 + 64p <= 65,
+//          Y3 = (R D + Y1 (4p - PPP)) / R'  (one reduction for both
+//          products) <= M
 //   add:   P, R <= 5.01 (+4p), the rest as madd
-//   dbl:   U = 2Y <= 10.02, M = 3X^2 <= 3.03, X3, Y3 as madd
-// Largest product of operand bounds: 17 x 33 = 561 << 2^24.
+//   dbl:   U = 2Y <= 8.02, M = 3X^2 <= 3.03, X3, Y3 as madd
+// Largest product of operand bounds: 65 x 65 = 4225 << 2^24.
 // Exceptional cases (P = 0 mod p: doubling or inverse) are detected on PP =
 // P^2, a product output, whose low limb screens them behind a branch that
 // waves almost never take.  The identity is the all-zero ZZ marker.
@@ -25,21 +27,25 @@ ECG_DEV bool xyzz_is_zero_rr(const XYZZ<FpR<Q>>& p) {
   return fis_zero(p.ZZ);
 }
 
-// mdbl-2008-s-1: 2 (x, y), x <= M, y <= 4p
+// dbl-2008-s-1 core on (X, Y) with the new ZZ, ZZZ factors V = U^2, W = U V
+template <class Q>
+ECG_DEV void rr_dbl_core(const FpR<Q>& X, const FpR<Q>& Y, XYZZ<FpR<Q>>& r, FpR<Q>& V, FpR<Q>& W) {
+  using F = FpR<Q>;
+  const F U = rr_add(Y, Y);
+  F S, X2;
+  V = rr_sqr(U);
+  rr_mul2(U, V, X, V, W, S);
+  X2 = rr_sqr(X);
+  const F Mm = rr_add(rr_add(X2, X2), X2);
+  r.X = rr_sub2<16>(rr_sqr(Mm), S, S);
+  r.Y = rr_mul_sum2(Mm, rr_sub<64>(S, r.X), Y, rr_neg<4>(W));
+}
+
+// mdbl-2008-s-1: 2 (x, y)
 template <class Q>
 ECG_DEV XYZZ<FpR<Q>> rr_dbl_affine(const Affine<FpR<Q>>& a) {
-  using F = FpR<Q>;
-  const F U = rr_add(a.y, a.y);
-  const F V = rr_sqr(U);
-  const F W = rr_mul(U, V);
-  const F S = rr_mul(a.x, V);
-  const F X2 = rr_sqr(a.x);
-  const F Mm = rr_add(rr_add(X2, X2), X2);
-  XYZZ<F> r;
-  r.X = rr_sub<8>(rr_sqr(Mm), rr_add(S, S));
-  r.Y = rr_sub<4>(rr_mul(Mm, rr_sub<32>(S, r.X)), rr_mul(W, a.y));
-  r.ZZ = V;
-  r.ZZZ = W;
+  XYZZ<FpR<Q>> r;
+  rr_dbl_core(a.x, a.y, r, r.ZZ, r.ZZZ);
   return r;
 }
 
@@ -48,60 +54,57 @@ template <class Q>
 ECG_DEV XYZZ<FpR<Q>> rr_dbl(const XYZZ<FpR<Q>>& p) {
   using F = FpR<Q>;
   if (xyzz_is_zero_rr(p)) return p;
-  const F U = rr_add(p.Y, p.Y);
-  const F V = rr_sqr(U);
-  const F W = rr_mul(U, V);
-  const F S = rr_mul(p.X, V);
-  const F X2 = rr_sqr(p.X);
-  const F Mm = rr_add(rr_add(X2, X2), X2);
   XYZZ<F> r;
-  r.X = rr_sub<8>(rr_sqr(Mm), rr_add(S, S));
-  r.Y = rr_sub<4>(rr_mul(Mm, rr_sub<32>(S, r.X)), rr_mul(W, p.Y));
-  r.ZZ = rr_mul(V, p.ZZ);
-  r.ZZZ = rr_mul(W, p.ZZZ);
+  F V, W;
+  rr_dbl_core(p.X, p.Y, r, V, W);
+  rr_mul2(V, p.ZZ, W, p.ZZZ, r.ZZ, r.ZZZ);
   return r;
 }
 
-// madd-2008-s: P + (x2, y2); `a` must not be the identity.  The ten
-// products run as five independent pairs (rr_mul2 / rr_sqr2).
+// madd-2008-s: P + (x2, y2); `a` must not be the identity (a.y may be wide).
+// Products run as independent pairs (rr_mul2 / rr_sqr2) plus one product sum.
 template <class Q>
 ECG_DEV XYZZ<FpR<Q>> rr_add_affine(const XYZZ<FpR<Q>>& p, const Affine<FpR<Q>>& a) {
   using F = FpR<Q>;
   if (xyzz_is_zero_rr(p)) {
     XYZZ<F> r;
     r.X = a.x;
-    r.Y = a.y;
+    r.Y = rr_carry<Q>(a.y.v);  // stored points are QN
     r.ZZ = F::one();
     r.ZZZ = F::one();
     return r;
   }
-  F U2, S2, PP, RR, PPP, Qv, T, Y3b;
+  F U2, S2, PP, RR, PPP, Qv;
   rr_mul2(a.x, p.ZZ, a.y, p.ZZZ, U2, S2);
-  const F P = rr_sub<32>(U2, p.X);
+  const F P = rr_sub<64>(U2, p.X);
   const F R = rr_sub<16>(S2, p.Y);
   rr_sqr2(P, R, PP, RR);
   rr_mul2(P, PP, p.X, PP, PPP, Qv);
   XYZZ<F> r;
   rr_mul2(p.ZZ, PP, p.ZZZ, PPP, r.ZZ, r.ZZZ);
-  r.X = rr_sub<8>(RR, rr_add(rr_add(PPP, Qv), Qv));
-  rr_mul2(R, rr_sub<32>(Qv, r.X), p.Y, PPP, T, Y3b);
-  r.Y = rr_sub<4>(T, Y3b);
+  r.X = rr_sub3<16>(RR, PPP, Qv, Qv);
+  r.Y = rr_mul_sum2(R, rr_sub<64>(Qv, r.X), p.Y, rr_neg<4>(PPP));
   if (rr_maybe_zero_prod(PP)) {  // rare: P = Q or P = -Q
     if (rr_is_zero_prod(PP)) {
-      if (rr_is_zero_prod(RR)) return rr_dbl_affine(a);
+      if (rr_is_zero_prod(RR)) {
+        Affine<F> b;
+        b.x = a.x;
+        b.y = rr_carry<Q>(a.y.v);
+        return rr_dbl_affine(b);
+      }
       return xyzz_zero<F>();
     }
   }
   return r;
 }
 
-// add-2008-s: P + Q (seven product pairs)
+// add-2008-s: P + Q
 template <class Q>
 ECG_DEV XYZZ<FpR<Q>> rr_add_xyzz(const XYZZ<FpR<Q>>& p, const XYZZ<FpR<Q>>& q) {
   using F = FpR<Q>;
   if (xyzz_is_zero_rr(p)) return q;
   if (xyzz_is_zero_rr(q)) return p;
-  F U1, U2, S1, S2, PP, RR, PPP, Qv, ZZ12, ZZZ12, T, Y3b;
+  F U1, U2, S1, S2, PP, RR, PPP, Qv, ZZ12, ZZZ12;
   rr_mul2(p.X, q.ZZ, q.X, p.ZZ, U1, U2);
   rr_mul2(p.Y, q.ZZZ, q.Y, p.ZZZ, S1, S2);
   const F P = rr_sub<4>(U2, U1);
@@ -111,9 +114,8 @@ ECG_DEV XYZZ<FpR<Q>> rr_add_xyzz(const XYZZ<FpR<Q>>& p, const XYZZ<FpR<Q>>& q) {
   rr_mul2(p.ZZ, q.ZZ, p.ZZZ, q.ZZZ, ZZ12, ZZZ12);
   XYZZ<F> r;
   rr_mul2(ZZ12, PP, ZZZ12, PPP, r.ZZ, r.ZZZ);
-  r.X = rr_sub<8>(RR, rr_add(rr_add(PPP, Qv), Qv));
-  rr_mul2(R, rr_sub<32>(Qv, r.X), S1, PPP, T, Y3b);
-  r.Y = rr_sub<4>(T, Y3b);
+  r.X = rr_sub3<16>(RR, PPP, Qv, Qv);
+  r.Y = rr_mul_sum2(R, rr_sub<64>(Qv, r.X), S1, rr_neg<4>(PPP));
   if (rr_maybe_zero_prod(PP)) {
     if (rr_is_zero_prod(PP)) {
       if (rr_is_zero_prod(RR)) return rr_dbl(p);
@@ -155,14 +157,15 @@ ECG_DEV XYZZ<FpR<Q>> pa_dbl(const XYZZ<FpR<Q>>& p) {
   return rr_dbl(p);
 }
 
-// negated base y (y <= M)
+// negated base y (y <= M); the reduced-radix form stays wide (no carry
+// step): it only meets product outputs in rr_add_affine
 template <class F>
 ECG_DEV F pa_neg_y(const F& y) {
   return fneg_lz(y);
 }
 template <class Q>
 ECG_DEV FpR<Q> pa_neg_y(const FpR<Q>& y) {
-  return rr_neg<4>(y);
+  return rr_neg_wide<4>(y);
 }
 
 // k P for a small unsigned k (double-and-add from the MSB)

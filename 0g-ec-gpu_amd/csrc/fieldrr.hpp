@@ -167,6 +167,51 @@ ECG_DEV void rr_mul2(const FpR<Q>& a0, const FpR<Q>& b0, const FpR<Q>& a1, const
   r1.v[NL - 1] = (uint32_t)x1;
 }
 
+ECG_DEV void mad64x2ss(uint64_t& acc0, uint32_t a0, uint32_t b0_uniform, uint64_t& acc1, uint32_t a1,
+                       uint32_t b1_uniform) {
+  uint64_t c0, c1;
+  asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %6, %7, %1"
+      : "+v"(acc0), "+v"(acc1), "=&s"(c0), "=&s"(c1)
+      : "v"(a0), "s"(b0_uniform), "v"(a1), "s"(b1_uniform));
+}
+
+// (a b + c d) / R': one Montgomery reduction for a sum of two products (all
+// four operands QN; a column holds 3 NL products < 3 * 14 * 2^58 < 2^64).
+// Two accumulators per column (a b | c d, the m p terms split between them)
+// merged before the digit.
+template <class Q>
+ECG_DEV FpR<Q> rr_mul_sum2(const FpR<Q>& a, const FpR<Q>& b, const FpR<Q>& c, const FpR<Q>& d) {
+  constexpr int NL = Q::NL, B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  uint32_t m[NL];
+  FpR<Q> r;
+  uint64_t x0 = 0, x1 = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * NL - 1; k++) {
+    const int i0 = k < NL ? 0 : k - NL + 1;
+    const int i1 = k < NL ? k : NL - 1;
+#pragma unroll
+    for (int i = i0; i <= i1; i++) mad64x2(x0, a.v[i], b.v[k - i], x1, c.v[i], d.v[k - i]);
+    const int j1 = k < NL ? k - 1 : NL - 1;  // m[j] p[k-j], j in [i0, j1]
+    int j = i0;
+#pragma unroll
+    for (; j + 1 <= j1; j += 2) mad64x2ss(x0, m[j], Q::P[k - j], x1, m[j + 1], Q::P[k - j - 1]);
+    if (j == j1) mad64s(x0, m[j], Q::P[k - j]);
+    x0 += x1;
+    x1 = 0;
+    if (k < NL) {
+      m[k] = ((uint32_t)x0 * Q::INV) & MASK;
+      mad64s(x0, m[k], Q::P[0]);
+    } else {
+      r.v[k - NL] = (uint32_t)x0 & MASK;
+    }
+    x0 >>= B;
+  }
+  r.v[NL - 1] = (uint32_t)x0;
+  return r;
+}
+
 // r0 = a0^2 / R', r1 = a1^2 / R'
 template <class Q>
 ECG_DEV void rr_sqr2(const FpR<Q>& a0, const FpR<Q>& a1, FpR<Q>& r0, FpR<Q>& r1) {
@@ -285,6 +330,42 @@ ECG_DEV FpR<Q> rr_neg(const FpR<Q>& a) {
 #pragma unroll
   for (int i = 0; i < Q::NL; i++) s[i] = Q::KP[j][i] - a.v[i];
   return rr_carry<Q>(s);
+}
+
+// a + K p - b - c - d  (deep-borrowed K p; requires b + c + d <= K p / 2):
+// three subtractions, one carry step
+template <int K, class Q>
+ECG_DEV FpR<Q> rr_sub3(const FpR<Q>& a, const FpR<Q>& b, const FpR<Q>& c, const FpR<Q>& d) {
+  constexpr int j = kp_index<K>();
+  static_assert((Q::KPD_OK >> j) & 1, "K p (deep borrow) not representable for this field");
+  uint32_t s[Q::NL];
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) s[i] = a.v[i] + Q::KPD[j][i] - b.v[i] - c.v[i] - d.v[i];
+  return rr_carry<Q>(s);
+}
+
+// a + K p - b - c
+template <int K, class Q>
+ECG_DEV FpR<Q> rr_sub2(const FpR<Q>& a, const FpR<Q>& b, const FpR<Q>& c) {
+  constexpr int j = kp_index<K>();
+  static_assert((Q::KPD_OK >> j) & 1, "K p (deep borrow) not representable for this field");
+  uint32_t s[Q::NL];
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) s[i] = a.v[i] + Q::KPD[j][i] - b.v[i] - c.v[i];
+  return rr_carry<Q>(s);
+}
+
+// K p - a WITHOUT the carry step ("wide": limbs < 2^(BITS+1) + 2^BITS).  Only
+// for an operand of rr_mul / rr_mul2 whose partner is a product output: the
+// column then stays below 14 * 2^59.6 + 14 * 2^58 < 2^64.
+template <int K, class Q>
+ECG_DEV FpR<Q> rr_neg_wide(const FpR<Q>& a) {
+  constexpr int j = kp_index<K>();
+  static_assert((Q::KP_OK >> j) & 1, "K p not representable for this field (tools/gen_params_rr.py)");
+  FpR<Q> r;
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) r.v[i] = Q::KP[j][i] - a.v[i];
+  return r;
 }
 
 // exact all-zero limbs (the identity marker; never a product output of a

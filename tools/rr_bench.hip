@@ -66,6 +66,10 @@ __global__ void k_check(const Fp<typename Q::Base>* x, const Fp<typename Q::Base
     e |= !feq(rr_to_std(u), fmul(a, a)) || !feq(rr_to_std(w), fmul(b, b)) ? 256u : 0u;
   }
   e |= !feq(rr_to_std(rr_sub<4>(ra, rb)), fsub(a, b)) ? 8u : 0u;
+  e |= !feq(rr_to_std(rr_mul_sum2(ra, rb, rb, rr_neg<4>(ra))), fsub(fmul(a, b), fmul(b, a))) ? 512u : 0u;
+  e |= !feq(rr_to_std(rr_mul_sum2(ra, rb, ra, ra)), fadd(fmul(a, b), fmul(a, a))) ? 1024u : 0u;
+  e |= !feq(rr_to_std(rr_sub3<16>(ra, rb, rb, ra)), fsub(fsub(fsub(a, b), b), a)) ? 2048u : 0u;
+  e |= !feq(rr_to_std(rr_mul(rr_neg_wide<4>(ra), rr_mul(rb, rb))), fmul(fneg(a), fmul(b, b))) ? 4096u : 0u;
   e |= !feq(rr_to_std(rr_neg<4>(ra)), fneg(a)) ? 16u : 0u;
   // a lazy chain: (a - b + 64p-ish) squared and multiplied stays congruent
   FpR<Q> big = rr_sub<32>(rr_sub<32>(ra, rb), rb);
