@@ -38,6 +38,7 @@
 //                     GPU lane (host_field.hpp).
 #pragma once
 #include <hipcub/hipcub.hpp>
+#include <rocprim/rocprim.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -69,6 +70,35 @@ static uint32_t msm_red_seg() {  // buckets per reduction segment
 static uint32_t msm_acc_seg() {  // sorted entries per accumulation thread
   static uint32_t v = env_u32("ECG_MSM_ACC_SEG", 128);
   return v;
+}
+
+static bool msm_pw_enabled() {  // A/B switch: ECG_MSM_PW=0 keeps one global sort
+  static const bool v = env_u32("ECG_MSM_PW", 1) != 0;
+  return v;
+}
+static int msm_sort_cfg() {  // onesweep config of the per-block sorts (A/B: ECG_MSM_SORTCFG)
+  static const int v = (int)env_u32("ECG_MSM_SORTCFG", 2);
+  return v;
+}
+
+// rocPRIM onesweep radix sort of (u32 key, u32 value) pairs over bits [b0, b1).
+// cfg 0: rocPRIM's tuned gfx950 config (8-bit digits); 1, 2: 10-bit digits
+// (1024-thread blocks, 8 / 12 items per thread): 20-bit block keys in 2 passes.
+using SortCfg10a = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+using SortCfg10b = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 12>, rocprim::kernel_config<1024, 12>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+static hipError_t msm_sort(int cfg, void* tmp, size_t& bytes, const uint32_t* ki, uint32_t* ko, const uint32_t* vi,
+                           uint32_t* vo, size_t n, int b0, int b1, hipStream_t s) {
+  switch (cfg) {
+    case 1: return rocprim::radix_sort_pairs<SortCfg10a>(tmp, bytes, ki, ko, vi, vo, n, b0, b1, s);
+    case 2: return rocprim::radix_sort_pairs<SortCfg10b>(tmp, bytes, ki, ko, vi, vo, n, b0, b1, s);
+    default: return rocprim::radix_sort_pairs(tmp, bytes, ki, ko, vi, vo, n, b0, b1, s);
+  }
 }
 
 struct MsmPlan {
@@ -178,32 +208,58 @@ ECG_DEV int32_t window_digit(const uint32_t* s, uint32_t w, const MsmPlan& pl, u
   return d;
 }
 
+// Key layout of the sorted (key, value) entries.
+//  * global (kc = 0): key = group*B + |d|-1, zero digits get the sentinel G*B;
+//    one sort over every entry (bits [0, log2(G*B+1))).
+//  * window-padded (kc = c): each (window, line) block of m entries is padded
+//    to mpad (a multiple of the accumulation segment) and keyed
+//    group << c | local, local = |d|-1 or the block sentinel B (zero digits and
+//    padding).  Every block is sorted on its own over bits [0, c) -- for c = 20
+//    two 10-bit onesweep passes instead of three 8-bit passes over 23 bits --
+//    measured 4 ms faster at 2^26.  Blocks align with segments, so a segment
+//    never spans two blocks.
+struct KeyMap {
+  uint32_t kc;        // 0 = global keys, else c
+  uint32_t B;         // buckets per group
+  uint32_t sentinel;  // global mode: the sentinel key G*B
+  ECG_DEV bool sent(uint32_t k) const { return kc ? (k & B) != 0 : k >= sentinel; }  // KEY_END too
+  ECG_DEV uint32_t bucket(uint32_t k) const { return kc ? (k >> kc) * B + (k & (B - 1)) : k; }
+};
+
 // One thread per scalar j of the row; the digits are emitted once per line
-// (entry (w, line, j) -> key = group(line, chunk(j), w) * B + |d| - 1).
+// (entry (w, line, j) at ((w * n_lines + line) * mpad + j)).
 template <class C>
 __global__ void __launch_bounds__(MSM_THREADS)
-    msm_digits_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, uint32_t* __restrict__ keys,
-                      uint32_t* __restrict__ vals) {
+    msm_digits_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, size_t mpad, KeyMap km,
+                      uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const size_t m = (size_t)g.n_chunks * g.clen;
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= m) return;
+  if (j >= mpad) return;
+  if (j >= m) {  // block padding (window-padded mode only): block sentinels
+    for (uint32_t w = 0; w < pl.W; w++)
+      for (uint32_t l = 0; l < g.n_lines; l++) {
+        const size_t o = ((size_t)w * g.n_lines + l) * mpad + j;
+        keys[o] = ((l * pl.W + w) << km.kc) | km.B;
+        vals[o] = 0;
+      }
+    return;
+  }
   uint32_t s[9];
   load_scalar<C>(scalars, j, g.scalar_mont, s);
   const uint32_t chunk = g.n_chunks == 1 ? 0u : (uint32_t)(j / g.clen);
-  const uint32_t sentinel = pl.G * pl.B;
   uint32_t carry = 0;
   for (uint32_t w = 0; w < pl.W; w++) {
     const int32_t d = window_digit(s, w, pl, carry);
     const uint32_t mag = d < 0 ? (uint32_t)(-d) : (uint32_t)d;
     const uint32_t sign = d < 0 ? 0x80000000u : 0u;
     for (uint32_t l = 0; l < g.n_lines; l++) {
-      const size_t o = ((size_t)w * g.n_lines + l) * m + j;
+      const size_t o = ((size_t)w * g.n_lines + l) * mpad + j;
+      const uint32_t grp = (l * g.n_chunks + chunk) * pl.W + w;
       if (d == 0) {
-        keys[o] = sentinel;
+        keys[o] = km.kc ? (grp << km.kc) | km.B : km.sentinel;
         vals[o] = 0;
       } else {
-        const uint32_t grp = (l * g.n_chunks + chunk) * pl.W + w;
-        keys[o] = grp * pl.B + (mag - 1);
+        keys[o] = km.kc ? (grp << km.kc) | (mag - 1) : grp * pl.B + (mag - 1);
         vals[o] = (uint32_t)(l * g.line_len + j) | sign;
       }
     }
@@ -234,15 +290,17 @@ constexpr uint32_t KEY_END = 0xffffffffu;
 template <class F>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
     msm_accumulate_kernel(const F* __restrict__ bases, const uint32_t* __restrict__ keys,
-                          const uint32_t* __restrict__ vals, size_t total, uint32_t sentinel, uint32_t seg,
-                          XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ recs, uint32_t* __restrict__ rkeys) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+                          const uint32_t* __restrict__ vals, size_t total, KeyMap km, uint32_t seg, size_t t0,
+                          size_t t1, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ recs,
+                          uint32_t* __restrict__ rkeys) {
+  const size_t t = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // segment
+  if (t >= t1) return;
   const size_t e0 = t * seg;
   if (e0 >= total) return;
   const size_t e1 = e0 + seg < total ? e0 + seg : total;
   const XYZZ<F> zero = xyzz_zero<F>();
   uint32_t b = keys[e0];
-  if (b >= sentinel) {  // all-zero-digit tail: no records
+  if (km.sent(b)) {  // all-zero-digit tail: no records
     store_xyzz(&recs[2 * t], zero);
     store_xyzz(&recs[2 * t + 1], zero);
     rkeys[2 * t] = KEY_END;
@@ -258,30 +316,31 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
     const bool more = e + 1 < e1;
     const uint32_t kn = more ? keys[e + 1] : KEY_END;
     const uint32_t vn = more ? vals[e + 1] : 0u;
+    const bool last = km.sent(kn);  // end of segment or of the block's non-zero digits
     Affine<F> Pn;
-    if (kn < sentinel) Pn = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
+    if (!last) Pn = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
     if (!aff_is_identity(P)) {  // GpuRepr identity (impls.rs:52-54) contributes nothing
       F ny = pa_neg_y(P.y);  // k p - y: one subtraction (lazy range)
       if (v >> 31) P.y = ny;
       acc = pa_add_affine(acc, P);
     }
     if (kn != b) {
-      const bool last = kn >= sentinel;  // end of segment or of the non-zero digits
+      const uint32_t bi = km.bucket(b);
       if (first_run) {
         store_xyzz(&recs[2 * t], acc);
-        rkeys[2 * t] = b;
+        rkeys[2 * t] = bi;
         if (last) {
           store_xyzz(&recs[2 * t + 1], zero);
-          rkeys[2 * t + 1] = b;
+          rkeys[2 * t + 1] = bi;
           return;
         }
         first_run = false;
       } else if (last) {
         store_xyzz(&recs[2 * t + 1], acc);
-        rkeys[2 * t + 1] = b;
+        rkeys[2 * t + 1] = bi;
         return;
       } else {
-        store_xyzz(&buckets[b], acc);  // interior run: a whole bucket
+        store_xyzz(&buckets[bi], acc);  // interior run: a whole bucket
       }
       acc = zero;
       b = kn;
@@ -305,45 +364,39 @@ __global__ void __launch_bounds__(MSM_THREADS)
     msm_combine_kernel(const XYZZ<F>* __restrict__ rin, const uint32_t* __restrict__ kin, size_t n,
                        uint32_t sentinel, uint32_t seg, int final_level, XYZZ<F>* __restrict__ buckets,
                        XYZZ<F>* __restrict__ rout, uint32_t* __restrict__ kout) {
+  // Record keys are bucket indices or KEY_END (identity records of all-zero
+  // segments).  Runs of one key are contiguous; KEY_END runs may sit between
+  // blocks (window-padded mode), so they are carried along, never stored.
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t e0 = t * seg;
   if (e0 >= n) return;
   const size_t e1 = e0 + seg < n ? e0 + seg : n;
   const XYZZ<F> zero = xyzz_zero<F>();
   uint32_t b = kin[e0];
-  if (b >= sentinel) {
-    if (!final_level) {
-      store_xyzz(&rout[2 * t], zero);
-      store_xyzz(&rout[2 * t + 1], zero);
-      kout[2 * t] = KEY_END;
-      kout[2 * t + 1] = KEY_END;
-    }
-    return;
-  }
   XYZZ<F> acc = zero;
   bool first_run = true;
   for (size_t e = e0; e < e1; e++) {
-    const uint32_t kn = e + 1 < e1 ? kin[e + 1] : KEY_END;
-    acc = pa_add(acc, load_xyzz(&rin[e]));
-    if (kn != b) {
-      const bool last = kn >= sentinel;
+    const bool end = e + 1 == e1;
+    const uint32_t kn = end ? KEY_END : kin[e + 1];
+    if (b < sentinel) acc = pa_add(acc, load_xyzz(&rin[e]));
+    if (end || kn != b) {
       if (final_level) {
-        store_xyzz(&buckets[b], acc);
-        if (last) return;
+        if (b < sentinel) store_xyzz(&buckets[b], acc);
+        if (end) return;
       } else if (first_run) {
         store_xyzz(&rout[2 * t], acc);
         kout[2 * t] = b;
-        if (last) {
+        if (end) {
           store_xyzz(&rout[2 * t + 1], zero);
           kout[2 * t + 1] = b;
           return;
         }
         first_run = false;
-      } else if (last) {
+      } else if (end) {
         store_xyzz(&rout[2 * t + 1], acc);
         kout[2 * t + 1] = b;
         return;
-      } else {
+      } else if (b < sentinel) {
         store_xyzz(&buckets[b], acc);
       }
       acc = zero;
@@ -556,9 +609,16 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   using F = AF;
   using X = XYZZ<F>;
   const size_t m = (size_t)g.n_chunks * g.clen;  // scalars consumed
-  const size_t total = (size_t)pl.W * g.n_lines * m;
   const uint32_t nb = pl.G * pl.B;
   const uint32_t sentinel = nb;
+  // window-padded keys (KeyMap) when every (window, line) block is one group
+  // and large enough for a sort of its own
+  const bool pw = msm_pw_enabled() && g.n_chunks == 1 && m >= ((size_t)1 << 16) &&
+                  ((uint64_t)pl.G << pl.c) < 0xffffffffull;
+  const size_t mpad = pw ? (m + pl.seg - 1) / pl.seg * pl.seg : m;
+  const size_t nblk = (size_t)pl.W * g.n_lines;
+  const size_t total = nblk * mpad;
+  const KeyMap km{pw ? pl.c : 0u, pl.B, sentinel};
   int key_bits = 1;
   while ((1ull << key_bits) <= sentinel) key_bits++;
   const size_t nseg = (total + pl.seg - 1) / pl.seg;
@@ -577,21 +637,24 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
   ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * pl.S / MSM_FOLD + pl.G) * sizeof(X), &pb));
 
+  hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(mpad, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                     (const uint4*)d_scalars, g, pl, mpad, km, (uint32_t*)k0, (uint32_t*)v0);
+  ECG_HIP(hipGetLastError());
+
   // ---- group the (key, value) entries by bucket: rocPRIM onesweep radix sort
   // (an MSD counting sort with 10-bit coarse bins was measured 3x slower:
   // 13K bins leave ~0.15 entries per bin per tile, so its scatter cannot
   // coalesce -- onesweep's 8-bit digits exist for exactly that reason)
-  const size_t ntot = total;
-  hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(m, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     (const uint4*)d_scalars, g, pl, (uint32_t*)k0, (uint32_t*)v0);
-  ECG_HIP(hipGetLastError());
+  const int cfg = pw ? msm_sort_cfg() : 0;
+  const size_t sort_n = pw ? mpad : total;  // one sort per block, or one global sort
+  const int sort_bits = pw ? (int)pl.c : key_bits;
   size_t tmp_bytes = 0;
-  ECG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
-                                             (uint32_t*)v1, total, 0, key_bits, s));
+  ECG_HIP(msm_sort(cfg, nullptr, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0, (uint32_t*)v1, sort_n, 0,
+                   sort_bits, s));
   ECG_TRY(ws_get(ctx, "msm_sort_tmp", tmp_bytes, &tmp));
-  ECG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (uint32_t*)k0, (uint32_t*)k1, (uint32_t*)v0,
-                                             (uint32_t*)v1, total, 0, key_bits, s));
-  const size_t nseg_used = (ntot + pl.seg - 1) / pl.seg;
+  for (size_t o = 0; o < total; o += sort_n)
+    ECG_HIP(msm_sort(cfg, tmp, tmp_bytes, (uint32_t*)k0 + o, (uint32_t*)k1 + o, (uint32_t*)v0 + o,
+                     (uint32_t*)v1 + o, sort_n, 0, sort_bits, s));
 
   // buckets nobody writes (no term) stay the identity: all-zero XYZZ (ZZ = 0)
   ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X), s));
@@ -607,15 +670,19 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     bases = (const F*)rb;
   }
 
+  // one launch over every segment: per-block launches, each started as soon
+  // as its block was sorted on a second stream, measured 6 ms slower at 2^26
+  // (13 launch tails, and the concurrent sort slows the VALU-bound
+  // accumulation by as much as it hides)
   ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
-  hipLaunchKernelGGL(msm_accumulate_kernel<F>, dim3(blocks_for(nseg_used, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     bases, (const uint32_t*)k1, (const uint32_t*)v1, ntot, sentinel, pl.seg, (X*)bk,
-                     (X*)rc, (uint32_t*)rk);
+  hipLaunchKernelGGL(msm_accumulate_kernel<F>, dim3(blocks_for(nseg, MSM_THREADS)), dim3(MSM_THREADS), 0, s, bases,
+                     (const uint32_t*)k1, (const uint32_t*)v1, total, km, pl.seg, (size_t)0, nseg, (X*)bk, (X*)rc,
+                     (uint32_t*)rk);
   ECG_HIP(hipGetLastError());
   ECG_TRY(kt_end(ctx, "msm_accumulate", s));
 
   // combine the segment-edge partials, level by level
-  size_t nrec = 2 * nseg_used;
+  size_t nrec = 2 * nseg;
   X* rin = (X*)rc;
   uint32_t* kin = (uint32_t*)rk;
   X* rout = (X*)rc2;
