@@ -279,6 +279,23 @@ __global__ void __launch_bounds__(MSM_THREADS)
 // holes.  msm_combine_kernel sums the records level by level.
 constexpr uint32_t KEY_END = 0xffffffffu;
 
+// r = c ? s : r limb by limb (Fp, FpR, Fp2).  A whole-struct `if (c) r = s`
+// can become a copy through a selected pointer, i.e. via scratch memory.
+template <class P>
+ECG_DEV void limb_sel(Fp<P>& r, bool c, const Fp<P>& s) {
+#pragma unroll
+  for (int i = 0; i < Fp<P>::L; i++) r.v[i] = c ? s.v[i] : r.v[i];
+}
+template <class Q>
+ECG_DEV void limb_sel(FpR<Q>& r, bool c, const FpR<Q>& s) {
+  rr_sel(r, c, s);
+}
+template <class P>
+ECG_DEV void limb_sel(Fp2<P>& r, bool c, const Fp2<P>& s) {
+  limb_sel(r.c0, c, s.c0);
+  limb_sel(r.c1, c, s.c1);
+}
+
 // Occupancy hint for the accumulate kernel (A/B: -DECG_ACC_WAVES=n sets
 // amdgpu_waves_per_eu(n), i.e. a VGPR budget of 512/n per lane).
 #ifdef ECG_ACC_WAVES
@@ -317,11 +334,15 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
     const uint32_t kn = more ? keys[e + 1] : KEY_END;
     const uint32_t vn = more ? vals[e + 1] : 0u;
     const bool last = km.sent(kn);  // end of segment or of the block's non-zero digits
+#ifndef ECG_ACC_NOPREFETCH
     Affine<F> Pn;
     if (!last) Pn = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
+#endif
     if (!aff_is_identity(P)) {  // GpuRepr identity (impls.rs:52-54) contributes nothing
-      F ny = pa_neg_y(P.y);  // k p - y: one subtraction (lazy range)
-      if (v >> 31) P.y = ny;
+      const F ny = pa_neg_y(P.y);  // k p - y: one subtraction (lazy range)
+      // per-limb select: a whole-struct `if (neg) P.y = ny` lets the compiler
+      // copy through a selected pointer, i.e. via scratch memory
+      limb_sel(P.y, (v >> 31) != 0, ny);
       acc = pa_add_affine(acc, P);
     }
     if (kn != b) {
@@ -345,7 +366,11 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
       acc = zero;
       b = kn;
     }
+#ifndef ECG_ACC_NOPREFETCH
     P = Pn;
+#else
+    if (!last) P = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
+#endif
     v = vn;
   }
 }

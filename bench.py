@@ -38,7 +38,6 @@ sys.path.insert(0, os.path.join(ROOT, "0g-ec-gpu_amd"))
 import ecgpu  # noqa: E402  (product path: libecgpu.so, fails loudly if missing)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
-MAD_PEAK_T = 35.3              # measured v_mad_u64_u32 lane-ops/s, T/s (tools/mad_microbench.hip)
 R_BLS = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 R_BN = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
 P_BLS = int("1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab", 16)
@@ -47,9 +46,37 @@ MSM_SEED = 0x35A00026
 NTT_SEED = 0x0FF70024
 KAT_A = 0x1234567890ABCDEF1122334455667788
 KAT_B = 0x0FEDCBA987654321
-# v_mad_u64_u32 per Fq multiplication (2 L^2, L = 32-bit limbs) and per Fr mul
-MADS_FQ = {0: 2 * 12 * 12, 1: 2 * 8 * 8}
-MADS_FR = 2 * 8 * 8
+# VALU roofs (the kernels are VALU-bound; AMD publishes no integer-MAD rate, so
+# these are measured field-product rates on MI355X):
+#  * MSM accumulation: 10 Fq products per term per window (madd-2008-s, 8M+2S)
+#    in the reduced-radix form; roof = the 8M+2S mix of the paired product /
+#    squaring rates (tools/rr_bench.hip, profiles/r01d/rr_bench.log).
+#  * NTT: exact Fr products per transform (ntt_fr_muls) vs the 32-bit-limb Fr
+#    product rate (tools/field_bench.hip, profiles/r01/field_bench_ilp2.log).
+FQ_MIX_PEAK_G = {0: 10 / (8 / 76.89 + 2 / 93.95), 1: 10 / (8 / 144.55 + 2 / 172.14)}
+FR_MUL_PEAK_G = 132.65
+
+
+def ntt_fr_muls(log_n: int, max_deg: int = 10) -> float:
+    """Fr products of one radix-2^d Stockham NTT as ntt.hip runs it: balanced
+    passes of <= max_deg, radix-2^2 DIF steps (a quartet costs 1 + 3 (h-1)/h
+    products: twiddles with qm = 0 are skipped), odd last round trivial, and
+    one inter-pass twiddle per element with a non-zero exponent."""
+    npass = -(-log_n // max_deg)
+    degs = [log_n // npass + (1 if k < log_n % npass else 0) for k in range(npass)]
+    n = 1 << log_n
+    total, lgp = 0.0, 0
+    for k, d in enumerate(degs):
+        R = 1 << d
+        r = 0
+        while r + 1 < d:
+            h = (R >> 2) >> r
+            total += n / 4 * (1 + 3 * (h - 1) / h)
+            r += 2
+        if k > 0:
+            total += n * (1 - 1 / (1 << lgp)) * (1 - 1 / R)
+        lgp += d
+    return total
 
 
 def parse():
@@ -372,10 +399,17 @@ def main():
         "aux": aux,
     }
     if W:
-        mads = n_loc * W * 10 * MADS_FQ[cid]
-        line["valu"] = {"kernel": "msm_accumulate", "mad_tops": mads / (acc_avg_ms / 1e3) / 1e12,
-                        "mad_peak_tops": MAD_PEAK_T, "frac": mads / (acc_avg_ms / 1e3) / 1e12 / MAD_PEAK_T,
-                        "note": "v_mad_u64_u32 issued for 10 Fq muls per term per window (c=20)"}
+        acc_step_ms = acc_ms / args.steps  # every accumulation launch of one MSM
+        rate = n_loc * W * 10 / (acc_step_ms / 1e3) / 1e9
+        line["valu"] = {"kernel": "msm_accumulate", "achieved": rate, "peak": FQ_MIX_PEAK_G[cid],
+                        "unit": "G Fq-mul/s", "frac": rate / FQ_MIX_PEAK_G[cid],
+                        "note": "10 Fq products (8M+2S) per term per window (c=20) / accumulation time, "
+                                "vs the measured reduced-radix 8M+2S product rate"}
+    muls = ntt_fr_muls(log_n)
+    fr_rate = muls / (pass_ms / args.steps / 1e3) / 1e9
+    line["ntt"]["valu"] = {"kernel": "ntt_pass", "achieved": fr_rate, "peak": FR_MUL_PEAK_G,
+                           "unit": "G Fr-mul/s", "frac": fr_rate / FR_MUL_PEAK_G,
+                           "note": f"{muls / n_ntt:.2f} Fr products per element per transform / kernel time"}
     print(json.dumps(line))
     if world > 1:
         dist.barrier()
