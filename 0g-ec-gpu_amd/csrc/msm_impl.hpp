@@ -433,21 +433,77 @@ __global__ void __launch_bounds__(MSM_THREADS)
 // ---------------------------------------------------------------------------
 // 5. per-segment summation by parts
 // ---------------------------------------------------------------------------
+// Two kernels: the running sums, then the segment offsets (sgm LS) run_s.
+// One point of each chain is parked in LDS between its uses (word-major, one
+// column per lane: conflict-free): with run, acc, the loaded bucket and the
+// add's temporaries all in VGPRs these kernels needed > 256 registers and ran
+// at 1 wave/SIMD.
+// 2 waves/SIMD at the price of a small spill (A/B: -DECG_RED_W1 lets the
+// compiler pick 1 wave/SIMD without spills)
+#ifdef ECG_RED_W1
+#define ECG_RED_ATTR
+#else
+#define ECG_RED_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
+#endif
+
 template <class F>
-__global__ void __launch_bounds__(MSM_THREADS)
-    msm_reduce_kernel(const XYZZ<F>* __restrict__ buckets, MsmPlan pl, XYZZ<F>* __restrict__ partial) {
+struct LdsPoint {  // XYZZ<F> words of lane t at w[i * MSM_THREADS + t]
+  uint32_t* w;
+  static constexpr int NW = (int)(sizeof(XYZZ<F>) / 4);
+  ECG_DEV void put(const XYZZ<F>& p) const {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(&p);
+#pragma unroll
+    for (int i = 0; i < NW; i++) w[i * MSM_THREADS + threadIdx.x] = s[i];
+  }
+  ECG_DEV XYZZ<F> get() const {
+    XYZZ<F> p;
+    uint32_t* d = reinterpret_cast<uint32_t*>(&p);
+#pragma unroll
+    for (int i = 0; i < NW; i++) d[i] = w[i * MSM_THREADS + threadIdx.x];
+    return p;
+  }
+};
+
+template <class F>
+__global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
+    msm_reduce_kernel(const XYZZ<F>* __restrict__ buckets, MsmPlan pl, XYZZ<F>* __restrict__ partial,
+                      XYZZ<F>* __restrict__ runs) {
+  __shared__ uint32_t lds[LdsPoint<F>::NW * MSM_THREADS];
+  const LdsPoint<F> acc_l{lds};
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= pl.G * pl.S) return;
   const uint32_t w = id / pl.S, sgm = id % pl.S;
   const XYZZ<F>* bk = buckets + (size_t)w * pl.B + (size_t)sgm * pl.LS;
-  XYZZ<F> run = xyzz_zero<F>(), acc = xyzz_zero<F>();
+  XYZZ<F> run = xyzz_zero<F>();
+  acc_l.put(xyzz_zero<F>());
   for (int j = (int)pl.LS - 1; j >= 0; j--) {
     run = pa_add(run, load_xyzz(&bk[j]));
-    acc = pa_add(acc, run);
+    acc_l.put(pa_add(acc_l.get(), run));
   }
-  // acc = sum_j (j+1) S_j ; add (sgm*LS) * run for the segment offset
-  if (sgm != 0) acc = pa_add(acc, pa_mul_small(run, sgm * pl.LS));
-  store_xyzz(&partial[id], acc);
+  // acc = sum_j (j+1) S_j ; run = sum_j S_j
+  store_xyzz(&partial[id], acc_l.get());
+  store_xyzz(&runs[id], run);
+}
+
+// partial[id] += (sgm LS) run_sgm  (segment offset of the bucket weights)
+template <class F>
+__global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
+    msm_reduce_offset_kernel(const XYZZ<F>* __restrict__ runs, MsmPlan pl, XYZZ<F>* __restrict__ partial) {
+  __shared__ uint32_t lds[LdsPoint<F>::NW * MSM_THREADS];
+  const LdsPoint<F> base{lds};
+  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= pl.G * pl.S) return;
+  const uint32_t sgm = id % pl.S;
+  if (sgm == 0) return;
+  const uint32_t k = sgm * pl.LS;  // double-and-add from the MSB; the base waits in LDS
+  const XYZZ<F> p = load_xyzz(&runs[id]);
+  base.put(p);
+  XYZZ<F> acc = p;
+  for (int b = 30 - __builtin_clz(k); b >= 0; b--) {
+    acc = pa_dbl(acc);
+    if ((k >> b) & 1) acc = pa_add(acc, base.get());
+  }
+  store_xyzz(&partial[id], pa_add(load_xyzz(&partial[id]), acc));
 }
 
 // ---------------------------------------------------------------------------
@@ -725,8 +781,13 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     std::swap(kin, kout);
   }
 
+  void* runs;
+  ECG_TRY(ws_get(ctx, "msm_runs", (size_t)pl.G * pl.S * sizeof(X), &runs));
   hipLaunchKernelGGL(msm_reduce_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
-                     dim3(MSM_THREADS), 0, s, (const X*)bk, pl, (X*)pa);
+                     dim3(MSM_THREADS), 0, s, (const X*)bk, pl, (X*)pa, (X*)runs);
+  ECG_HIP(hipGetLastError());
+  hipLaunchKernelGGL(msm_reduce_offset_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
+                     dim3(MSM_THREADS), 0, s, (const X*)runs, pl, (X*)pa);
   ECG_HIP(hipGetLastError());
 
   uint32_t cnt = pl.S;
