@@ -279,6 +279,27 @@ __global__ void __launch_bounds__(MSM_THREADS)
 // holes.  msm_combine_kernel sums the records level by level.
 constexpr uint32_t KEY_END = 0xffffffffu;
 
+// Affine base [x, y] records as the accumulation gathers them: the boundary
+// layout (2 Fq, packed) or, in the reduced-radix form, padded to whole 128-B
+// lines (112 B -> 128 B for BLS12-381): an unaligned 112-B record straddles
+// two lines for most bases, which doubled the gather traffic (PMC FETCH_SIZE).
+template <class F>
+struct BaseLayout {
+  static constexpr size_t BYTES = 2 * sizeof(F);
+};
+template <class Q>
+struct BaseLayout<FpR<Q>> {
+  static constexpr size_t BYTES = (2 * sizeof(FpR<Q>) + 127) / 128 * 128;
+};
+template <class F>
+ECG_HD const F* base_ptr(const F* bases, size_t i) {
+  return reinterpret_cast<const F*>(reinterpret_cast<const char*>(bases) + i * BaseLayout<F>::BYTES);
+}
+template <class F>
+ECG_HD F* base_ptr(F* bases, size_t i) {
+  return reinterpret_cast<F*>(reinterpret_cast<char*>(bases) + i * BaseLayout<F>::BYTES);
+}
+
 // r = c ? s : r limb by limb (Fp, FpR, Fp2).  A whole-struct `if (c) r = s`
 // can become a copy through a selected pointer, i.e. via scratch memory.
 template <class P>
@@ -325,7 +346,7 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
     return;
   }
   uint32_t v = vals[e0];
-  Affine<F> P = load_affine(bases + 2 * (size_t)(v & 0x7fffffffu));
+  Affine<F> P = load_affine(base_ptr(bases, v & 0x7fffffffu));
   XYZZ<F> acc = zero;
   bool first_run = true;
   for (size_t e = e0; e < e1; e++) {
@@ -336,7 +357,7 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
     const bool last = km.sent(kn);  // end of segment or of the block's non-zero digits
 #ifndef ECG_ACC_NOPREFETCH
     Affine<F> Pn;
-    if (!last) Pn = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
+    if (!last) Pn = load_affine(base_ptr(bases, vn & 0x7fffffffu));
 #endif
     if (!aff_is_identity(P)) {  // GpuRepr identity (impls.rs:52-54) contributes nothing
       const F ny = pa_neg_y(P.y);  // k p - y: one subtraction (lazy range)
@@ -369,7 +390,7 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
 #ifndef ECG_ACC_NOPREFETCH
     P = Pn;
 #else
-    if (!last) P = load_affine(bases + 2 * (size_t)(vn & 0x7fffffffu));
+    if (!last) P = load_affine(base_ptr(bases, vn & 0x7fffffffu));
 #endif
     v = vn;
   }
@@ -541,7 +562,7 @@ __global__ void __launch_bounds__(MSM_THREADS)
     r.x = rr_from_std<Q>(a.x);
     r.y = rr_from_std<Q>(a.y);
   }
-  store_affine(out + 2 * i, r);
+  store_affine(base_ptr(out, i), r);
 }
 
 template <class F, class FS>
@@ -718,6 +739,21 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
   ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * pl.S / MSM_FOLD + pl.G) * sizeof(X), &pb));
 
+  // buckets nobody writes (no term) stay the identity: all-zero XYZZ (ZZ = 0).
+  // (Running this clear and the base conversion on a side stream, concurrent
+  // with the digits and the sorts, measured no gain: all are HBM-bound.)
+  ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X), s));
+  const F* bases = (const F*)d_bases;
+  if constexpr (!std::is_same<F, typename C::Fq>::value) {
+    const size_t nb_in = (size_t)g.n_lines * g.line_len;  // every base a value can index
+    void* rb;
+    ECG_TRY(ws_get(ctx, "msm_rr_bases", nb_in * BaseLayout<F>::BYTES, &rb));
+    hipLaunchKernelGGL(msm_rr_bases_kernel<typename F::Params>, dim3(blocks_for(nb_in, MSM_THREADS)),
+                       dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, nb_in, (F*)rb);
+    ECG_HIP(hipGetLastError());
+    bases = (const F*)rb;
+  }
+
   hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(mpad, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
                      (const uint4*)d_scalars, g, pl, mpad, km, (uint32_t*)k0, (uint32_t*)v0);
   ECG_HIP(hipGetLastError());
@@ -736,20 +772,6 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   for (size_t o = 0; o < total; o += sort_n)
     ECG_HIP(msm_sort(cfg, tmp, tmp_bytes, (uint32_t*)k0 + o, (uint32_t*)k1 + o, (uint32_t*)v0 + o,
                      (uint32_t*)v1 + o, sort_n, 0, sort_bits, s));
-
-  // buckets nobody writes (no term) stay the identity: all-zero XYZZ (ZZ = 0)
-  ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X), s));
-
-  const F* bases = (const F*)d_bases;
-  if constexpr (!std::is_same<F, typename C::Fq>::value) {
-    const size_t nb_in = (size_t)g.n_lines * g.line_len;  // every base a value can index
-    void* rb;
-    ECG_TRY(ws_get(ctx, "msm_rr_bases", nb_in * 2 * sizeof(F), &rb));
-    hipLaunchKernelGGL(msm_rr_bases_kernel<typename F::Params>, dim3(blocks_for(nb_in, MSM_THREADS)),
-                       dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, nb_in, (F*)rb);
-    ECG_HIP(hipGetLastError());
-    bases = (const F*)rb;
-  }
 
   // one launch over every segment: per-block launches, each started as soon
   // as its block was sorted on a second stream, measured 6 ms slower at 2^26
