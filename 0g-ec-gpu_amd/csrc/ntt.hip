@@ -62,6 +62,12 @@ ECG_DEV F twiddle(const F* __restrict__ tw_lo, const F* __restrict__ tw_hi, uint
 //   u[i] = x[g + i*t] * w^((n >> (lgp+DEG)) * k * i),  k = g mod 2^lgp, t = n >> DEG
 //   y[(g - k)*2^DEG + k + j*2^lgp] = v[j]   (v = DFT of u, natural order)
 // ---------------------------------------------------------------------------
+// A thread owns at most NTT_EPT elements of the tile (launch: threads >= E /
+// NTT_EPT).  Every global load of the tile -- elements and twiddles -- is
+// issued before the first product, so a tile waits for one HBM latency, not
+// one per element (the strided loop over a runtime bound could not unroll).
+constexpr int NTT_EPT = 4;
+
 template <class F, int DEG>
 ECG_DEV void pass_load(const F* __restrict__ x, const F* __restrict__ tw_lo, const F* __restrict__ tw_hi,
                        const F* __restrict__ twf, const LdsPlanes<F>& U, uint32_t log_n, uint32_t lgp,
@@ -71,20 +77,35 @@ ECG_DEV void pass_load(const F* __restrict__ x, const F* __restrict__ tw_lo, con
   const uint64_t p = 1ull << lgp;
   const uint64_t g0 = (uint64_t)blockIdx.x << log_g;
   const uint32_t s_tw_log = log_n - lgp - DEG;  // n >> (lgp + DEG) = 2^s_tw_log
-  for (uint32_t f = threadIdx.x; f < E; f += blockDim.x) {
-    const uint32_t gi = f & (G - 1), i = f >> log_g;
-    const uint64_t g = g0 + gi;
-    F v = load(&x[g + (uint64_t)i * t]);
-    if (lgp != 0) {
-      const uint64_t k = g & (p - 1);
-      const uint64_t e = (k * i) << s_tw_log;  // < n
-      if (e != 0) {
-        // full per-pass table twf[i * p + k] (one load, k contiguous across
-        // lanes) or the split tables (two loads + one product)
-        v = fmul(v, twf ? load(&twf[(uint64_t)i * p + k]) : twiddle(tw_lo, tw_hi, e));
+  F v[NTT_EPT], w[NTT_EPT];
+  bool mul[NTT_EPT];
+#pragma unroll
+  for (int q = 0; q < NTT_EPT; q++) {
+    const uint32_t f = threadIdx.x + q * blockDim.x;
+    mul[q] = false;
+    if (f < E) {
+      const uint32_t gi = f & (G - 1), i = f >> log_g;
+      const uint64_t g = g0 + gi;
+      v[q] = load(&x[g + (uint64_t)i * t]);
+      if (lgp != 0) {
+        const uint64_t k = g & (p - 1);
+        const uint64_t e = (k * i) << s_tw_log;  // < n
+        if (e != 0) {
+          // full per-pass table twf[i * p + k] (one load, k contiguous across
+          // lanes) or the split tables (two loads + one product)
+          mul[q] = true;
+          w[q] = twf ? load(&twf[(uint64_t)i * p + k]) : twiddle(tw_lo, tw_hi, e);
+        }
       }
     }
-    U.put((gi << DEG) + i, v);
+  }
+#pragma unroll
+  for (int q = 0; q < NTT_EPT; q++) {
+    const uint32_t f = threadIdx.x + q * blockDim.x;
+    if (f < E) {
+      if (mul[q]) v[q] = fmul(v[q], w[q]);
+      U.put(((f & (G - 1)) << DEG) + (f >> log_g), v[q]);
+    }
   }
 }
 
@@ -95,7 +116,10 @@ ECG_DEV void pass_store(F* __restrict__ y, const LdsPlanes<F>& U, uint32_t lgp, 
   const uint64_t g0 = (uint64_t)blockIdx.x << log_g;
   const uint32_t lpp = lgp < log_g ? lgp : log_g;  // lanes walk min(p, G) fastest -> contiguous runs
   const uint32_t pp = 1u << lpp;
-  for (uint32_t f = threadIdx.x; f < E; f += blockDim.x) {
+#pragma unroll
+  for (int q = 0; q < NTT_EPT; q++) {
+    const uint32_t f = threadIdx.x + q * blockDim.x;
+    if (f >= E) break;
     const uint32_t kk = f & (pp - 1);
     const uint32_t j = (f >> lpp) & (R - 1);
     const uint32_t gh = f >> (lpp + DEG);
@@ -111,7 +135,7 @@ ECG_DEV void pass_store(F* __restrict__ y, const LdsPlanes<F>& U, uint32_t lgp, 
 // ---------------------------------------------------------------------------
 // threads per workgroup = max(2^DEG, 1024) / 4 (see launch_pass)
 template <class P, int DEG>
-__global__ void __launch_bounds__(DEG >= 12 ? 1024 : DEG == 11 ? 512 : 256)
+__global__ void __launch_bounds__(1024)
     ntt_pass_kernel(const Fp<P>* __restrict__ x, Fp<P>* __restrict__ y, const Fp<P>* __restrict__ pq,
                     uint32_t pq_shift, const Fp<P>* __restrict__ tw_lo, const Fp<P>* __restrict__ tw_hi,
                     const Fp<P>* __restrict__ twf, uint32_t log_n, uint32_t lgp, uint32_t log_g) {
@@ -246,10 +270,18 @@ struct PassArgs {
   uint32_t log_n, lgp;
 };
 
+// A/B knob: log2 elements per workgroup (ECG_NTT_TILE, default 10)
+static uint32_t ntt_tile_log() {
+  static uint32_t v = [] {
+    const char* e = getenv("ECG_NTT_TILE");
+    return e ? (uint32_t)atoi(e) : 10u;
+  }();
+  return v;
+}
 template <class P, int DEG, bool V1>
 static hipError_t launch_pass(const PassArgs& a, hipStream_t s) {
   using F = Fp<P>;
-  const uint32_t tile_log = V1 ? 10 : (DEG > 10 ? DEG : 10);  // elements per workgroup
+  const uint32_t tile_log = V1 ? 10 : (DEG > ntt_tile_log() ? DEG : ntt_tile_log());  // elements per workgroup
   uint32_t log_g = tile_log - DEG;
   const uint32_t log_groups = a.log_n - DEG;
   if (log_g > log_groups) log_g = log_groups;
@@ -260,7 +292,7 @@ static hipError_t launch_pass(const PassArgs& a, hipStream_t s) {
   if (V1) {
     threads = 256;
   } else {
-    threads = E / 4;
+    threads = E / NTT_EPT;
     if (threads < 64) threads = 64;
     if (threads > 1024) threads = 1024;
   }
