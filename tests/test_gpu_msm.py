@@ -102,6 +102,20 @@ def test_msm_ragged_sizes(kernels, cname, cid):
                           co.multiexp_cpu(cid, B, E, nthreads=8)), n
 
 
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_ragged_window_padded(kernels, cname, cid):
+    """Sizes >= 2^16 take the window-padded key path (one sort per window
+    block, blocks padded to the 128-entry segment with sentinels): ragged
+    sizes put padding and zero digits inside segments and between blocks."""
+    cv = po.CURVES[cname]
+    for n in ((1 << 16) + 1, (1 << 16) + 37, 3 * (1 << 16) - 5):
+        B = co.gen_bases(cid, 1300 + n, 7, n, 8)
+        E = rand_scalars(cv, n, n)
+        E[::97] = 0  # zero scalars: sentinel entries in every window block
+        assert same_point(cid, kernels[cname].multiexp(ecgpu.Worker(), B, E, 0),
+                          co.multiexp_cpu(cid, B, E, nthreads=16)), n
+
+
 def test_msm_cycled_bases_and_scalars(kernels):
     """ag-cuda-ec/benches/multiexp.rs:24-26 inputs: bases cycled with period 99,
     scalars with period 73 -- heavy bucket skew and P + P additions."""
