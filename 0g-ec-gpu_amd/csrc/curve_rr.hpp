@@ -61,8 +61,6 @@ ECG_DEV XYZZ<FpR<Q>> rr_dbl(const XYZZ<FpR<Q>>& p) {
   return r;
 }
 
-// madd-2008-s: P + (x2, y2); `a` must not be the identity (a.y may be wide).
-// Products run as independent pairs (rr_mul2 / rr_sqr2) plus one product sum.
 // r = c ? s : r, limb by limb.  Results are merged this way (single exit, no
 // whole-struct assignment under a condition): a struct copy from a selected
 // source becomes a copy through a selected pointer, which pins both points
@@ -80,6 +78,8 @@ ECG_DEV void rr_sel(XYZZ<FpR<Q>>& r, bool c, const XYZZ<FpR<Q>>& s) {
   rr_sel(r.ZZZ, c, s.ZZZ);
 }
 
+// madd-2008-s: P + (x2, y2); `a` must not be the identity (a.y may be wide).
+// Products run as independent pairs (rr_mul2 / rr_sqr2) plus one product sum.
 template <class Q>
 ECG_DEV XYZZ<FpR<Q>> rr_add_affine(const XYZZ<FpR<Q>>& p, const Affine<FpR<Q>>& a) {
   using F = FpR<Q>;
@@ -178,6 +178,86 @@ ECG_DEV XYZZ<F> pa_dbl(const XYZZ<F>& p) {
 template <class Q>
 ECG_DEV XYZZ<FpR<Q>> pa_dbl(const XYZZ<FpR<Q>>& p) {
   return rr_dbl(p);
+}
+
+template <class F>
+ECG_DEV bool pa_is_zero(const XYZZ<F>& p) {
+  return xyzz_is_zero<F, true>(p);
+}
+template <class Q>
+ECG_DEV bool pa_is_zero(const XYZZ<FpR<Q>>& p) {
+  return xyzz_is_zero_rr(p);
+}
+
+// -P; the reduced-radix Y becomes 8p - Y (<= 8p): stored-point Y only ever
+// enters products (add-2008-s, dbl-2008-s-1), whose inputs have ample slack
+template <class F>
+ECG_DEV XYZZ<F> pa_neg(const XYZZ<F>& p) {
+  return xyzz_neg<F, true>(p);
+}
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> pa_neg(const XYZZ<FpR<Q>>& p) {
+  XYZZ<FpR<Q>> r = p;
+  r.Y = rr_neg<8>(p.Y);
+  return r;
+}
+
+// k P for a canonical 256-bit k (8 x u32), double-and-add from the top bit
+template <class F>
+ECG_DEV XYZZ<F> pa_mul_scalar(const XYZZ<F>& p, const uint32_t* k) {
+  int top = 255;
+  while (top >= 0 && !((k[top >> 5] >> (top & 31)) & 1)) top--;
+  if (top < 0 || pa_is_zero(p)) return xyzz_zero<F>();
+  XYZZ<F> acc = p;
+  for (int b = top - 1; b >= 0; b--) {
+    acc = pa_dbl(acc);
+    if ((k[b >> 5] >> (b & 31)) & 1) acc = pa_add(acc, p);
+  }
+  return acc;
+}
+
+// lazy 32-bit-limb XYZZ -> the pipeline's coordinate field
+template <class F>
+ECG_DEV XYZZ<F> pa_from_std(const XYZZ<F>& p) {
+  return p;
+}
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> pa_from_std_rr(const XYZZ<Fp<typename Q::Base>>& p) {
+  XYZZ<FpR<Q>> r;
+  r.X = rr_from_std<Q>(p.X);
+  r.Y = rr_from_std<Q>(p.Y);
+  r.ZZ = rr_from_std<Q>(p.ZZ);
+  r.ZZZ = rr_from_std<Q>(p.ZZZ);
+  return r;
+}
+
+// x * c for a boundary-form constant c (the GLV endomorphism's beta)
+template <class F>
+ECG_DEV F pa_mul_const(const F& x, const F& c) {
+  return fmul_lz(x, c);
+}
+template <class Q>
+ECG_DEV FpR<Q> pa_mul_const(const FpR<Q>& x, const Fp<typename Q::Base>& c) {
+  return rr_mul(x, rr_from_std<Q>(c));
+}
+
+// Coordinate field of the bucket / butterfly pipelines: the reduced-radix
+// form for the G1 base fields, the 32-bit-limb lazy form for G2 (Fq2).
+template <class FqP>
+struct RRof {
+  using Q = void;
+};
+template <>
+struct RRof<params::bls12_381_fq> {
+  using Q = params::bls12_381_fq_rr;
+};
+template <>
+struct RRof<params::bn254_fq> {
+  using Q = params::bn254_fq_rr;
+};
+template <class C>
+constexpr bool has_rr_form() {
+  return C::EXT == 1 && !std::is_same<typename RRof<typename C::FqParams>::Q, void>::value;
 }
 
 // negated base y (y <= M); the reduced-radix form stays wide (no carry

@@ -21,22 +21,38 @@
 //                      must be G1 (prime-order subgroup) points, as ark's
 //                      G1Projective values are.
 //   3. ecfft_stage     log_n launches of n/2 independent radix-2 DIT
-//                      butterflies (A, B) -> (A + wB, A - wB), lazy [0, 2p]
-//                      Fq arithmetic, w = 1 butterflies skip the multiply
+//                      butterflies (A, B) -> (A + wB, A - wB), w = 1
+//                      butterflies skip the multiply.  G1 points run in the
+//                      reduced-radix form of the MSM (curve_rr.hpp: converted
+//                      in ecfft_load, back in ecfft_store; ~1.5x faster than
+//                      the 32-bit-limb lazy form, which G2 keeps)
 //   4. ecfft_store     XYZZ -> normalised Jacobian (x, y, 1) / (0, 1, 0)
 #include <cstring>
 
 #include "ctx.hpp"
 #include "curve.hpp"
+#include "curve_rr.hpp"
 #include "dispatch.hpp"
 
 namespace ecg {
 
 constexpr int ECFFT_THREADS = 64;
 
-template <class C>
+
+// PF = coordinate field of the butterflies: C::Fq (32-bit limbs, lazy) or the
+// reduced-radix FpR of the G1 base fields (curve_rr.hpp)
+template <class C, class PF>
+ECG_DEV XYZZ<PF> to_pf(const XYZZ<typename C::Fq>& p) {
+  if constexpr (std::is_same<PF, typename C::Fq>::value) {
+    return p;
+  } else {
+    return pa_from_std_rr<typename PF::Params>(p);
+  }
+}
+
+template <class C, class PF>
 __global__ void __launch_bounds__(ECFFT_THREADS)
-    ecfft_load_kernel(const typename C::Fq* __restrict__ jac, uint32_t log_n, XYZZ<typename C::Fq>* __restrict__ a) {
+    ecfft_load_kernel(const typename C::Fq* __restrict__ jac, uint32_t log_n, XYZZ<PF>* __restrict__ a) {
   using F = typename C::Fq;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (1u << log_n)) return;
@@ -45,7 +61,7 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
   j.Y = load(&jac[3 * (size_t)i + 1]);
   j.Z = load(&jac[3 * (size_t)i + 2]);
   const uint32_t r = log_n ? (__brev(i) >> (32 - log_n)) : 0u;
-  store_xyzz(&a[r], xyzz_from_jac(j));
+  store_xyzz(&a[r], to_pf<C, PF>(xyzz_from_jac(j)));
 }
 
 template <class C>
@@ -118,27 +134,26 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
 // halves: one doubling per bit of the longer half and one full add from the
 // table {P, phi P, P + phi P} per nonzero bit pair.  The table lives in a
 // per-butterfly global slot (L2-resident), keeping VGPRs for the chain.
-template <class C>
-ECG_DEV XYZZ<typename C::Fq> glv_joint_mul(const XYZZ<typename C::Fq>& P, const uint32_t* k1, const uint32_t* k2,
-                                           XYZZ<typename C::Fq>* tab) {
+template <class C, class PF>
+ECG_DEV XYZZ<PF> glv_joint_mul(const XYZZ<PF>& P, const uint32_t* k1, const uint32_t* k2, XYZZ<PF>* tab) {
   using F = typename C::Fq;
-  if (xyzz_is_zero<F, true>(P)) return P;
+  if (pa_is_zero(P)) return P;
   F beta;
   from_u64_words(beta, C::Gen::BETA);
-  XYZZ<F> phi = P;
-  phi.X = fmul_lz(P.X, beta);
+  XYZZ<PF> phi = P;
+  phi.X = pa_mul_const(P.X, beta);
   store_xyzz(&tab[0], P);
   store_xyzz(&tab[1], phi);
-  store_xyzz(&tab[2], xyzz_add<F, true>(P, phi));
+  store_xyzz(&tab[2], pa_add(P, phi));
   int top = 127;
   while (top >= 0 && !(((k1[top >> 5] | k2[top >> 5]) >> (top & 31)) & 1)) top--;
-  if (top < 0) return xyzz_zero<F>();
+  if (top < 0) return xyzz_zero<PF>();
   const uint32_t d0 = ((k1[top >> 5] >> (top & 31)) & 1) | (((k2[top >> 5] >> (top & 31)) & 1) << 1);
-  XYZZ<F> acc = load_xyzz(&tab[d0 - 1]);
+  XYZZ<PF> acc = load_xyzz(&tab[d0 - 1]);
   for (int b = top - 1; b >= 0; b--) {
-    acc = xyzz_dbl<F, true>(acc);
+    acc = pa_dbl(acc);
     const uint32_t d = ((k1[b >> 5] >> (b & 31)) & 1) | (((k2[b >> 5] >> (b & 31)) & 1) << 1);
-    if (d) acc = xyzz_add<F, true>(acc, load_xyzz(&tab[d - 1]));
+    if (d) acc = pa_add(acc, load_xyzz(&tab[d - 1]));
   }
   return acc;
 }
@@ -146,40 +161,39 @@ ECG_DEV XYZZ<typename C::Fq> glv_joint_mul(const XYZZ<typename C::Fq>& P, const 
 // Stage s of the DIT: half-size h = 2^s; butterfly t pairs i0 = (t >> s) *
 // 2h + j and i1 = i0 + h, j = t mod h, twiddle omega^(j * n / 2h)
 // (serial_ec_fft's w = w_m^j, ec_fft_cpu.rs:35-49).
-template <class C>
+template <class C, class PF>
 __global__ void __launch_bounds__(ECFFT_THREADS)
-    ecfft_stage_kernel(XYZZ<typename C::Fq>* __restrict__ a, const uint4* __restrict__ tw, uint32_t log_n,
-                       uint32_t s, XYZZ<typename C::Fq>* __restrict__ glv_tab) {
-  using F = typename C::Fq;
+    ecfft_stage_kernel(XYZZ<PF>* __restrict__ a, const uint4* __restrict__ tw, uint32_t log_n, uint32_t s,
+                       XYZZ<PF>* __restrict__ glv_tab) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (1u << (log_n - 1))) return;
   const uint32_t h = 1u << s;
   const uint32_t j = t & (h - 1);
   const uint32_t i0 = ((t >> s) << (s + 1)) + j, i1 = i0 + h;
-  XYZZ<F> A = load_xyzz(&a[i0]);
-  XYZZ<F> B = load_xyzz(&a[i1]);
+  XYZZ<PF> A = load_xyzz(&a[i0]);
+  XYZZ<PF> B = load_xyzz(&a[i1]);
   if (j != 0) {
     const uint32_t e = j << (log_n - 1 - s);
     const uint4 lo = tw[2 * e], hi = tw[2 * e + 1];
     if constexpr (has_glv<C>()) {
       const uint32_t k1[4] = {lo.x, lo.y, lo.z, lo.w}, k2[4] = {hi.x, hi.y, hi.z, hi.w};
-      B = glv_joint_mul<C>(B, k1, k2, glv_tab + 3 * (size_t)t);
+      B = glv_joint_mul<C, PF>(B, k1, k2, glv_tab + 3 * (size_t)t);
     } else {
       const uint32_t k[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      B = xyzz_mul_scalar<F, true>(B, k);
+      B = pa_mul_scalar(B, k);
     }
   }
-  store_xyzz(&a[i0], xyzz_add<F, true>(A, B));
-  store_xyzz(&a[i1], xyzz_add<F, true>(A, xyzz_neg<F, true>(B)));
+  store_xyzz(&a[i0], pa_add(A, B));
+  store_xyzz(&a[i1], pa_add(A, pa_neg(B)));
 }
 
-template <class C>
+template <class C, class PF>
 __global__ void __launch_bounds__(ECFFT_THREADS)
-    ecfft_store_kernel(const XYZZ<typename C::Fq>* __restrict__ a, uint32_t n, typename C::Fq* __restrict__ jac) {
+    ecfft_store_kernel(const XYZZ<PF>* __restrict__ a, uint32_t n, typename C::Fq* __restrict__ jac) {
   using F = typename C::Fq;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  XYZZ<F> p = xyzz_canon(load_xyzz(&a[i]));
+  XYZZ<F> p = xyzz_canon(pa_to_std(load_xyzz(&a[i])));
   const bool id = xyzz_is_zero(p);
   Jac<F> j = jac_from_affine_norm(xyzz_to_affine(p), id);
   store(&jac[3 * (size_t)i], j.X);
@@ -189,20 +203,28 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
 
 static inline uint32_t ecfft_blocks(size_t n) { return (uint32_t)((n + ECFFT_THREADS - 1) / ECFFT_THREADS); }
 
-template <class C>
-static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
-                   ecg_abort_cb abort_cb, void* user) {
+static bool ecfft_rr_enabled() {  // A/B switch: ECG_ECFFT_RR=0 keeps the 32-bit-limb butterflies
+  static const bool v = [] {
+    const char* e = getenv("ECG_ECFFT_RR");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+template <class C, class PF>
+static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
+                    ecg_abort_cb abort_cb, void* user) {
   using F = typename C::Fq;
   using S = Fp<typename C::FrParams>;
   const uint32_t n = 1u << log_n;
   void *a, *tw, *gt = nullptr;
-  ECG_TRY(ws_get(ctx, "ecfft_pts", (size_t)n * sizeof(XYZZ<F>), &a));
+  ECG_TRY(ws_get(ctx, "ecfft_pts", (size_t)n * sizeof(XYZZ<PF>), &a));
   ECG_TRY(ws_get(ctx, "ecfft_tw", (size_t)(n / 2 + 1) * 32, &tw));
-  if (has_glv<C>()) ECG_TRY(ws_get(ctx, "ecfft_glv", (size_t)(n / 2 + 1) * 3 * sizeof(XYZZ<F>), &gt));
+  if (has_glv<C>()) ECG_TRY(ws_get(ctx, "ecfft_glv", (size_t)(n / 2 + 1) * 3 * sizeof(XYZZ<PF>), &gt));
   S om;
   memcpy(om.v, omega, sizeof(om.v));
-  hipLaunchKernelGGL(ecfft_load_kernel<C>, dim3(ecfft_blocks(n)), dim3(ECFFT_THREADS), 0, s, (const F*)d_jac, log_n,
-                     (XYZZ<F>*)a);
+  hipLaunchKernelGGL((ecfft_load_kernel<C, PF>), dim3(ecfft_blocks(n)), dim3(ECFFT_THREADS), 0, s, (const F*)d_jac, log_n,
+                     (XYZZ<PF>*)a);
   ECG_HIP(hipGetLastError());
   if (log_n > 0) {
     hipLaunchKernelGGL(ecfft_twiddle_kernel<C>, dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s, om, n / 2,
@@ -216,15 +238,25 @@ static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t lo
       return ECG_ABORTED;
     }
     ECG_TRY(kt_begin(ctx, "ecfft_stage", s));
-    hipLaunchKernelGGL(ecfft_stage_kernel<C>, dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s, (XYZZ<F>*)a,
-                       (const uint4*)tw, log_n, st, (XYZZ<F>*)gt);
+    hipLaunchKernelGGL((ecfft_stage_kernel<C, PF>), dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s,
+                       (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, (XYZZ<PF>*)gt);
     ECG_HIP(hipGetLastError());
     ECG_TRY(kt_end(ctx, "ecfft_stage", s));
   }
-  hipLaunchKernelGGL(ecfft_store_kernel<C>, dim3(ecfft_blocks(n)), dim3(ECFFT_THREADS), 0, s, (const XYZZ<F>*)a, n,
+  hipLaunchKernelGGL((ecfft_store_kernel<C, PF>), dim3(ecfft_blocks(n)), dim3(ECFFT_THREADS), 0, s, (const XYZZ<PF>*)a, n,
                      (F*)d_jac);
   ECG_HIP(hipGetLastError());
   return ECG_OK;
+}
+
+template <class C>
+static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
+                   ecg_abort_cb abort_cb, void* user) {
+  if constexpr (has_rr_form<C>()) {
+    if (ecfft_rr_enabled())
+      return ecfft_pf<C, FpR<typename RRof<typename C::FqParams>::Q>>(ctx, d_jac, omega, log_n, s, abort_cb, user);
+  }
+  return ecfft_pf<C, typename C::Fq>(ctx, d_jac, omega, log_n, s, abort_cb, user);
 }
 
 int ecfft_validate(int curve_id, uint32_t log_n) {

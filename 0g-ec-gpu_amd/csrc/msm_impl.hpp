@@ -562,7 +562,15 @@ __global__ void __launch_bounds__(MSM_THREADS)
     r.x = rr_from_std<Q>(a.x);
     r.y = rr_from_std<Q>(a.y);
   }
-  store_affine(base_ptr(out, i), r);
+  FpR<Q>* rec = base_ptr(out, i);
+  store_affine(rec, r);
+  // zero the record's pad too: whole-line writes (a partial line costs a
+  // read-modify-write; measured 3.3 -> 5.6 ms for this kernel without it)
+  constexpr size_t pad = BaseLayout<FpR<Q>>::BYTES - 2 * sizeof(FpR<Q>);
+  static_assert(pad % 16 == 0, "16-B vector stores");
+  uint4* tail = reinterpret_cast<uint4*>(reinterpret_cast<char*>(rec) + 2 * sizeof(FpR<Q>));
+#pragma unroll
+  for (size_t k = 0; k < pad / 16; k++) tail[k] = make_uint4(0, 0, 0, 0);
 }
 
 template <class F, class FS>
@@ -572,24 +580,6 @@ __global__ void msm_sums_to_std_kernel(const XYZZ<F>* __restrict__ in, uint32_t 
   store_xyzz(&out[i], pa_to_std(load_xyzz(&in[i])));
 }
 
-// Coordinate field of the bucket pipeline: the reduced-radix form for the G1
-// base fields, the 32-bit-limb lazy form for G2 (Fq2).
-template <class FqP>
-struct RRof {
-  using Q = void;
-};
-template <>
-struct RRof<params::bls12_381_fq> {
-  using Q = params::bls12_381_fq_rr;
-};
-template <>
-struct RRof<params::bn254_fq> {
-  using Q = params::bn254_fq_rr;
-};
-template <class C>
-constexpr bool msm_has_rr() {
-  return C::EXT == 1 && !std::is_same<typename RRof<typename C::FqParams>::Q, void>::value;
-}
 static bool msm_rr_enabled() {  // A/B switch: ECG_MSM_RR=0 runs the 32-bit-limb pipeline
   static const bool v = env_u32("ECG_MSM_RR", 1) != 0;
   return v;
@@ -842,7 +832,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
 template <class C>
 int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g, const MsmPlan& pl,
                hipStream_t s, void** d_sums) {
-  if constexpr (msm_has_rr<C>()) {
+  if constexpr (has_rr_form<C>()) {
     if (msm_rr_enabled())
       return msm_core_impl<C, FpR<typename RRof<typename C::FqParams>::Q>>(ctx, d_bases, d_scalars, g, pl, s,
                                                                             d_sums);
