@@ -13,7 +13,8 @@
 //                     applied to every window, carry-propagated), emits
 //                     (key = window*B + |d|-1, val = term | sign<<31).
 //  2. radix sort      (key, val) pairs, grouping each window's terms by bucket
-//                     (hipcub/rocPRIM onesweep).  Replaces the reference's
+//                     (rocPRIM onesweep; one 2-pass sort per window block of
+//                     window-padded keys, see KeyMap).  Replaces the reference's
 //                     per-thread global-memory bucket RMW (multiexp_backup.cl:45-58).
 //  3. msm_accumulate  fixed-length segments of SEG sorted entries per thread
 //                     (every lane runs exactly SEG XYZZ mixed adds, 8M+2S, of
@@ -23,13 +24,16 @@
 //                     are whole buckets and are stored; the first and last
 //                     run of each segment leave keyed partial records.
 //                     The dominant kernel: VALU-bound on v_mad_u64_u32.
+//                     G1 runs it in the reduced-radix form (curve_rr.hpp) on
+//                     bases converted to 128-B records (msm_rr_bases).
 //  4. msm_combine     the same fixed-segment scheme over the records, level
 //                     by level (32 records per thread, x16 fewer per level):
 //                     log-depth for any bucket skew.  Buckets without terms
 //                     keep the memset identity.
 //  5. msm_reduce      per window, 2^(c-1)/LS segments of LS buckets: running
-//                     sums (summation by parts, multiexp.cl:121-131) plus a
-//                     small-scalar multiple of the segment total.
+//                     sums (summation by parts, multiexp.cl:121-131); then
+//                     msm_reduce_offset adds the small-scalar multiple
+//                     (s LS) x (segment total).
 //  6. msm_sum         tree-fold of segment partials to one sum per window.
 //  7. host fold       Horner over windows (c doublings each) and the final
 //                     affine normalisation on the host -- the reference GPU
@@ -459,13 +463,18 @@ __global__ void __launch_bounds__(MSM_THREADS)
 // column per lane: conflict-free): with run, acc, the loaded bucket and the
 // add's temporaries all in VGPRs these kernels needed > 256 registers and ran
 // at 1 wave/SIMD.
-// 2 waves/SIMD at the price of a small spill (A/B: -DECG_RED_W1 lets the
-// compiler pick 1 wave/SIMD without spills)
-#ifdef ECG_RED_W1
-#define ECG_RED_ATTR
-#else
-#define ECG_RED_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
-#endif
+// Reduced-radix (G1) points: 2 waves/SIMD at the price of a small spill.
+// The Fq2 (G2) points keep the compiler's choice: forcing 2 waves would
+// spill ~600 B per lane.
+template <class F>
+struct RedWaves {
+  static constexpr int value = 1;
+};
+template <class Q>
+struct RedWaves<FpR<Q>> {
+  static constexpr int value = 2;
+};
+#define ECG_RED_ATTR __attribute__((amdgpu_waves_per_eu(RedWaves<F>::value)))
 
 template <class F>
 struct LdsPoint {  // XYZZ<F> words of lane t at w[i * MSM_THREADS + t]
