@@ -358,8 +358,10 @@ def main():
     # ------------------------------------------------------------ report
     bytes_per_term = 2 * lq * 8 + 32  # 96 B affine + 32 B scalar (BLS12-381), SURVEY §8(d)
     acc_achieved = bytes_per_term * n_loc / (acc_avg_ms / 1e3) / 1e9
-    acc_traffic, acc_src = pmc_traffic("msm_accumulate", streaming_read=False)
-    ntt_traffic, ntt_src = pmc_traffic("ntt_pass", streaming_read=True)
+    # the committed PMC passes profile the default (BLS12-381, 2^26 / 2^24) run
+    default_run = cid == 0 and args.msm_log == 26 and log_n == 24
+    acc_traffic, acc_src = pmc_traffic("msm_accumulate", streaming_read=False) if default_run else (None, None)
+    ntt_traffic, ntt_src = pmc_traffic("ntt_pass", streaming_read=True) if default_run else (None, None)
     ntt_achieved = 64 * n_ntt / (pass_avg_ms / 1e3) / 1e9
     # VALU evidence: v_mad_u64_u32 issued by the bucket accumulation (10 Fq muls
     # per XYZZ mixed add, one per term per window) vs the measured MAD roof.
