@@ -378,7 +378,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "u32-limb mod-p integer (v_mad_u64_u32)",
+        "dtype": "mod-p integer on v_mad_u64_u32 (MSM: 29-bit-limb reduced-radix Fq; NTT: u32-limb Fr)",
         "data": "synthetic: bases (a+i*b)G generated on GPU, scalars uniform < r (seeded), HBM-resident",
         "config": {"workload": f"{args.curve} G1 MSM 2^{args.msm_log} terms sharded over {world} GPU(s) "
                                f"+ Fr NTT 2^{log_n} per GPU", "msm_terms": n_total, "ntt_log_n": log_n,
