@@ -132,6 +132,67 @@ ECG_DEV void mad64x2s(uint64_t& acc0, uint32_t a0, uint64_t& acc1, uint32_t a1, 
       : "v"(a0), "v"(a1), "s"(b_uniform));
 }
 
+// Four mads -- two per chain -- per asm statement: half the statement
+// boundaries, after each of which the compiler places a hazard s_nop
+// (A/B: -DECG_RR_NO_X4 keeps two mads per statement).
+ECG_DEV void mad64x4(uint64_t& acc0, uint32_t a0, uint32_t b0, uint32_t c0, uint32_t d0, uint64_t& acc1, uint32_t a1,
+                     uint32_t b1, uint32_t c1, uint32_t d1) {
+  uint64_t k0, k1;
+  asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %8, %9, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %6, %7, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %10, %11, %1"
+      : "+v"(acc0), "+v"(acc1), "=&s"(k0), "=&s"(k1)
+      : "v"(a0), "v"(b0), "v"(c0), "v"(d0), "v"(a1), "v"(b1), "v"(c1), "v"(d1));
+}
+// acc0 += a0 u + c0 w, acc1 += a1 u + c1 w  (u, w uniform)
+ECG_DEV void mad64x4s(uint64_t& acc0, uint32_t a0, uint32_t c0, uint64_t& acc1, uint32_t a1, uint32_t c1, uint32_t u,
+                      uint32_t w) {
+  uint64_t k0, k1;
+  asm("v_mad_u64_u32 %0, %2, %4, %8, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %6, %8, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %5, %9, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %7, %9, %1"
+      : "+v"(acc0), "+v"(acc1), "=&s"(k0), "=&s"(k1)
+      : "v"(a0), "v"(c0), "v"(a1), "v"(c1), "s"(u), "s"(w));
+}
+
+// Column pieces of two interleaved products (k, lo, hi fold to constants in
+// the unrolled column loops): sum_{lo <= i <= hi} a_i b_{k-i} into (x0, x1),
+// and sum_{lo <= i <= hi} m_i P_{k-i} for the uniform modulus limbs P.
+ECG_DEV void col2(int k, int lo, int hi, uint64_t& x0, const uint32_t* a0, const uint32_t* b0, uint64_t& x1,
+                  const uint32_t* a1, const uint32_t* b1) {
+#pragma unroll
+  for (int i = lo; i <= hi; i += 2) {
+#ifndef ECG_RR_NO_X4
+    if (i + 1 <= hi) {
+      mad64x4(x0, a0[i], b0[k - i], a0[i + 1], b0[k - i - 1], x1, a1[i], b1[k - i], a1[i + 1], b1[k - i - 1]);
+      continue;
+    }
+#endif
+    mad64x2(x0, a0[i], b0[k - i], x1, a1[i], b1[k - i]);
+#ifdef ECG_RR_NO_X4
+    if (i + 1 <= hi) mad64x2(x0, a0[i + 1], b0[k - i - 1], x1, a1[i + 1], b1[k - i - 1]);
+#endif
+  }
+}
+template <class Q>
+ECG_DEV void col2p(int k, int lo, int hi, uint64_t& x0, const uint32_t* m0, uint64_t& x1, const uint32_t* m1) {
+#pragma unroll
+  for (int i = lo; i <= hi; i += 2) {
+#ifndef ECG_RR_NO_X4
+    if (i + 1 <= hi) {
+      mad64x4s(x0, m0[i], m0[i + 1], x1, m1[i], m1[i + 1], Q::P[k - i], Q::P[k - i - 1]);
+      continue;
+    }
+#endif
+    mad64x2s(x0, m0[i], x1, m1[i], Q::P[k - i]);
+#ifdef ECG_RR_NO_X4
+    if (i + 1 <= hi) mad64x2s(x0, m0[i + 1], x1, m1[i + 1], Q::P[k - i - 1]);
+#endif
+  }
+}
+
 // r0 = a0 b0 / R', r1 = a1 b1 / R'
 template <class Q>
 ECG_DEV void rr_mul2(const FpR<Q>& a0, const FpR<Q>& b0, const FpR<Q>& a1, const FpR<Q>& b1, FpR<Q>& r0,
@@ -142,10 +203,8 @@ ECG_DEV void rr_mul2(const FpR<Q>& a0, const FpR<Q>& b0, const FpR<Q>& a1, const
   uint64_t x0 = 0, x1 = 0;
 #pragma unroll
   for (int k = 0; k < NL; k++) {
-#pragma unroll
-    for (int i = 0; i <= k; i++) mad64x2(x0, a0.v[i], b0.v[k - i], x1, a1.v[i], b1.v[k - i]);
-#pragma unroll
-    for (int i = 0; i < k; i++) mad64x2s(x0, m0[i], x1, m1[i], Q::P[k - i]);
+    col2(k, 0, k, x0, a0.v, b0.v, x1, a1.v, b1.v);
+    col2p<Q>(k, 0, k - 1, x0, m0, x1, m1);
     m0[k] = ((uint32_t)x0 * Q::INV) & MASK;
     m1[k] = ((uint32_t)x1 * Q::INV) & MASK;
     mad64x2s(x0, m0[k], x1, m1[k], Q::P[0]);
@@ -154,10 +213,8 @@ ECG_DEV void rr_mul2(const FpR<Q>& a0, const FpR<Q>& b0, const FpR<Q>& a1, const
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
-#pragma unroll
-    for (int i = k - NL + 1; i < NL; i++) mad64x2(x0, a0.v[i], b0.v[k - i], x1, a1.v[i], b1.v[k - i]);
-#pragma unroll
-    for (int i = k - NL + 1; i < NL; i++) mad64x2s(x0, m0[i], x1, m1[i], Q::P[k - i]);
+    col2(k, k - NL + 1, NL - 1, x0, a0.v, b0.v, x1, a1.v, b1.v);
+    col2p<Q>(k, k - NL + 1, NL - 1, x0, m0, x1, m1);
     r0.v[k - NL] = (uint32_t)x0 & MASK;
     r1.v[k - NL] = (uint32_t)x1 & MASK;
     x0 >>= B;
@@ -191,8 +248,7 @@ ECG_DEV FpR<Q> rr_mul_sum2(const FpR<Q>& a, const FpR<Q>& b, const FpR<Q>& c, co
   for (int k = 0; k < 2 * NL - 1; k++) {
     const int i0 = k < NL ? 0 : k - NL + 1;
     const int i1 = k < NL ? k : NL - 1;
-#pragma unroll
-    for (int i = i0; i <= i1; i++) mad64x2(x0, a.v[i], b.v[k - i], x1, c.v[i], d.v[k - i]);
+    col2(k, i0, i1, x0, a.v, b.v, x1, c.v, d.v);
     const int j1 = k < NL ? k - 1 : NL - 1;  // m[j] p[k-j], j in [i0, j1]
     int j = i0;
 #pragma unroll
@@ -227,18 +283,15 @@ ECG_DEV void rr_sqr2(const FpR<Q>& a0, const FpR<Q>& a1, FpR<Q>& r0, FpR<Q>& r1)
 #pragma unroll
   for (int k = 0; k < 2 * NL - 1; k++) {
     const int i0 = k < NL ? 0 : k - NL + 1;
-#pragma unroll
-    for (int i = i0; 2 * i < k; i++) mad64x2(x0, d0[i], a0.v[k - i], x1, d1[i], a1.v[k - i]);
+    col2(k, i0, (k & 1) ? k / 2 : k / 2 - 1, x0, d0, a0.v, x1, d1, a1.v);  // 2 i < k
     if ((k & 1) == 0) mad64x2(x0, a0.v[k >> 1], a0.v[k >> 1], x1, a1.v[k >> 1], a1.v[k >> 1]);
     if (k < NL) {
-#pragma unroll
-      for (int i = 0; i < k; i++) mad64x2s(x0, m0[i], x1, m1[i], Q::P[k - i]);
+      col2p<Q>(k, 0, k - 1, x0, m0, x1, m1);
       m0[k] = ((uint32_t)x0 * Q::INV) & MASK;
       m1[k] = ((uint32_t)x1 * Q::INV) & MASK;
       mad64x2s(x0, m0[k], x1, m1[k], Q::P[0]);
     } else {
-#pragma unroll
-      for (int i = k - NL + 1; i < NL; i++) mad64x2s(x0, m0[i], x1, m1[i], Q::P[k - i]);
+      col2p<Q>(k, k - NL + 1, NL - 1, x0, m0, x1, m1);
       r0.v[k - NL] = (uint32_t)x0 & MASK;
       r1.v[k - NL] = (uint32_t)x1 & MASK;
     }
