@@ -157,11 +157,52 @@ ECG_DEV void mad64x4s(uint64_t& acc0, uint32_t a0, uint32_t c0, uint64_t& acc1, 
       : "v"(a0), "v"(c0), "v"(a1), "v"(c1), "s"(u), "s"(w));
 }
 
+// Eight mads -- four per chain -- per asm statement (A/B: -DECG_RR_X4_ONLY).
+ECG_DEV void mad64x8(uint64_t& acc0, const uint32_t* a0, const uint32_t* b0, uint64_t& acc1, const uint32_t* a1,
+                     const uint32_t* b1) {
+  uint64_t k0, k1;
+  asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %12, %13, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %6, %7, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %14, %15, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %8, %9, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %16, %17, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %10, %11, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %18, %19, %1"
+      : "+v"(acc0), "+v"(acc1), "=&s"(k0), "=&s"(k1)
+      : "v"(a0[0]), "v"(b0[0]), "v"(a0[1]), "v"(b0[1]), "v"(a0[2]), "v"(b0[2]), "v"(a0[3]), "v"(b0[3]),
+        "v"(a1[0]), "v"(b1[0]), "v"(a1[1]), "v"(b1[1]), "v"(a1[2]), "v"(b1[2]), "v"(a1[3]), "v"(b1[3]));
+}
+// acc0 += sum_t m0[t] u[t], acc1 += sum_t m1[t] u[t], t < 4 (u uniform)
+ECG_DEV void mad64x8s(uint64_t& acc0, const uint32_t* m0, uint64_t& acc1, const uint32_t* m1, const uint32_t* u) {
+  uint64_t k0, k1;
+  asm("v_mad_u64_u32 %0, %2, %4, %12, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %8, %12, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %5, %13, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %9, %13, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %6, %14, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %10, %14, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %7, %15, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %11, %15, %1"
+      : "+v"(acc0), "+v"(acc1), "=&s"(k0), "=&s"(k1)
+      : "v"(m0[0]), "v"(m0[1]), "v"(m0[2]), "v"(m0[3]), "v"(m1[0]), "v"(m1[1]), "v"(m1[2]), "v"(m1[3]),
+        "s"(u[0]), "s"(u[1]), "s"(u[2]), "s"(u[3]));
+}
+
 // Column pieces of two interleaved products (k, lo, hi fold to constants in
 // the unrolled column loops): sum_{lo <= i <= hi} a_i b_{k-i} into (x0, x1),
 // and sum_{lo <= i <= hi} m_i P_{k-i} for the uniform modulus limbs P.
 ECG_DEV void col2(int k, int lo, int hi, uint64_t& x0, const uint32_t* a0, const uint32_t* b0, uint64_t& x1,
                   const uint32_t* a1, const uint32_t* b1) {
+#if !defined(ECG_RR_NO_X4) && !defined(ECG_RR_X4_ONLY)
+  for (; lo + 3 <= hi; lo += 4) {
+    const uint32_t ta0[4] = {a0[lo], a0[lo + 1], a0[lo + 2], a0[lo + 3]};
+    const uint32_t tb0[4] = {b0[k - lo], b0[k - lo - 1], b0[k - lo - 2], b0[k - lo - 3]};
+    const uint32_t ta1[4] = {a1[lo], a1[lo + 1], a1[lo + 2], a1[lo + 3]};
+    const uint32_t tb1[4] = {b1[k - lo], b1[k - lo - 1], b1[k - lo - 2], b1[k - lo - 3]};
+    mad64x8(x0, ta0, tb0, x1, ta1, tb1);
+  }
+#endif
 #pragma unroll
   for (int i = lo; i <= hi; i += 2) {
 #ifndef ECG_RR_NO_X4
@@ -178,6 +219,14 @@ ECG_DEV void col2(int k, int lo, int hi, uint64_t& x0, const uint32_t* a0, const
 }
 template <class Q>
 ECG_DEV void col2p(int k, int lo, int hi, uint64_t& x0, const uint32_t* m0, uint64_t& x1, const uint32_t* m1) {
+#if !defined(ECG_RR_NO_X4) && !defined(ECG_RR_X4_ONLY)
+  for (; lo + 3 <= hi; lo += 4) {
+    const uint32_t t0[4] = {m0[lo], m0[lo + 1], m0[lo + 2], m0[lo + 3]};
+    const uint32_t t1[4] = {m1[lo], m1[lo + 1], m1[lo + 2], m1[lo + 3]};
+    const uint32_t u[4] = {Q::P[k - lo], Q::P[k - lo - 1], Q::P[k - lo - 2], Q::P[k - lo - 3]};
+    mad64x8s(x0, t0, x1, t1, u);
+  }
+#endif
 #pragma unroll
   for (int i = lo; i <= hi; i += 2) {
 #ifndef ECG_RR_NO_X4
