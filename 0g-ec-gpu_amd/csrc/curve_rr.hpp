@@ -33,9 +33,8 @@ ECG_DEV void rr_dbl_core(const FpR<Q>& X, const FpR<Q>& Y, XYZZ<FpR<Q>>& r, FpR<
   using F = FpR<Q>;
   const F U = rr_add(Y, Y);
   F S, X2;
-  V = rr_sqr(U);
+  rr_sqr2(U, X, V, X2);  // the two independent squarings as one interleaved pair
   rr_mul2(U, V, X, V, W, S);
-  X2 = rr_sqr(X);
   const F Mm = rr_add(rr_add(X2, X2), X2);
   r.X = rr_sub2<16>(rr_sqr(Mm), S, S);
   r.Y = rr_mul_sum2(Mm, rr_sub<64>(S, r.X), Y, rr_neg<4>(W));
