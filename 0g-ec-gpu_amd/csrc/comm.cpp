@@ -30,7 +30,11 @@ namespace ecg {
   } while (0)
 
 int comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes_per_peer, hipStream_t s) {
-  if (!ctx->comm || ctx->comm_size == 1) {  // one rank: the exchange is a copy
+  if (ctx->comm_size > 1 && !ctx->comm) {
+    set_error("comm_alltoall: %d ranks but no communicator", ctx->comm_size);
+    return ECG_ERR_RCCL;
+  }
+  if (ctx->comm_size == 1) {  // one rank: the exchange is a copy
     ECG_HIP(hipMemcpyAsync(d_recv, d_send, bytes_per_peer * ctx->comm_size, hipMemcpyDeviceToDevice, s));
     return ECG_OK;
   }
@@ -46,7 +50,11 @@ void comm_free(ecg_ctx* ctx) {
 }
 
 int comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes, hipStream_t s) {
-  if (!ctx->comm || ctx->comm_size == 1) {
+  if (ctx->comm_size > 1 && !ctx->comm) {
+    set_error("comm_allgather: %d ranks but no communicator", ctx->comm_size);
+    return ECG_ERR_RCCL;
+  }
+  if (ctx->comm_size == 1) {
     ECG_HIP(hipMemcpyAsync(d_recv, d_send, bytes, hipMemcpyDeviceToDevice, s));
     return ECG_OK;
   }
@@ -72,23 +80,20 @@ int ecg_comm_unique_id(uint8_t* out) {
 }
 
 int ecg_comm_init(ecg_ctx* ctx, int nranks, int rank, const uint8_t* unique_id) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (nranks < 1 || rank < 0 || rank >= nranks || (!unique_id && nranks > 1)) {
     set_error("ecg_comm_init: bad arguments (nranks %d, rank %d)", nranks, rank);
     return ECG_ERR_INVALID;
   }
-  if (ctx->comm) {
-    (void)ncclCommDestroy((ncclComm_t)ctx->comm);
-    ctx->comm = nullptr;
-  }
-  ctx->comm_size = nranks;
-  ctx->comm_rank = rank;
+  comm_free(ctx);  // back to the single-rank state until the new communicator exists
   if (nranks == 1) return ECG_OK;
   ncclUniqueId id;
   memcpy(id.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
   ncclComm_t c;
   ECG_NCCL(ncclCommInitRank(&c, nranks, id, rank));
   ctx->comm = c;
+  ctx->comm_size = nranks;
+  ctx->comm_rank = rank;
   return ECG_OK;
 }
 
@@ -100,14 +105,14 @@ void ecg_comm_destroy(ecg_ctx* ctx) {
 }
 
 int ecg_comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   ECG_TRY(comm_allgather(ctx, d_send, d_recv, bytes, ctx->stream));
   ECG_HIP(hipStreamSynchronize(ctx->stream));
   return ECG_OK;
 }
 
 int ecg_comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes_per_peer) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   ECG_TRY(comm_alltoall(ctx, d_send, d_recv, bytes_per_peer, ctx->stream));
   ECG_HIP(hipStreamSynchronize(ctx->stream));
   return ECG_OK;
@@ -117,7 +122,7 @@ int ecg_comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t byt
 // RCCL and folded, so every rank returns the full result.
 int ecg_msm_dist(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n_local,
                  uint64_t* out_jac) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!out_jac || ((!d_bases || !d_scalars) && n_local)) {
     set_error("ecg_msm_dist: null pointer");
     return ECG_ERR_INVALID;
@@ -145,7 +150,7 @@ int ecg_msm_dist(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_
 // One NTT of 2^log_n points block-distributed over the communicator's ranks
 // (this rank holds points [rank*m, (rank+1)*m), m = 2^log_n / size); in place.
 int ecg_fft_dist(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omega, uint32_t log_n) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!d_local || !omega) {
     set_error("ecg_fft_dist: null pointer");
     return ECG_ERR_INVALID;
@@ -159,7 +164,7 @@ int ecg_fft_dist(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omeg
 // several contexts on one device) can drive the exchanges itself.
 int ecg_fft_dist_stage1(ecg_ctx* ctx, int field_id, const void* d_in, void* d_out, const uint64_t* omega,
                         uint32_t nranks, uint32_t rank, uint32_t log_n) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!d_in || !d_out || !omega) {
     set_error("ecg_fft_dist_stage1: null pointer");
     return ECG_ERR_INVALID;
@@ -170,7 +175,7 @@ int ecg_fft_dist_stage1(ecg_ctx* ctx, int field_id, const void* d_in, void* d_ou
 }
 
 int ecg_fft_dist_stage3(ecg_ctx* ctx, const void* d_in, void* d_out, uint32_t nranks, uint32_t log_n) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!d_in || !d_out) {
     set_error("ecg_fft_dist_stage3: null pointer");
     return ECG_ERR_INVALID;

@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -36,6 +37,14 @@ void set_error(const char* fmt, ...);
     if (rc_ != ECG_OK) return rc_; \
   } while (0)
 
+// Entry of every API call on a context: make its device current and hold the
+// context's lock for the rest of the call (one context may be shared by
+// several host threads -- e.g. listed twice in ecg_msm_multi's ctxs -- so its
+// stream, workspace map and event pool are never used concurrently).
+#define ECG_ENTER(ctx)                                   \
+  ECG_TRY(::ecg::ctx_enter(ctx));                        \
+  std::lock_guard<std::recursive_mutex> ecg_ctx_lock_((ctx)->mu)
+
 struct KernelTimes {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   double ms = 0.0;
@@ -47,6 +56,7 @@ struct KernelTimes {
 struct ecg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  std::recursive_mutex mu;  // held by every API call on this context (ECG_ENTER)
   size_t mem_bytes = 0;
   int compute_units = 0;
   struct Buf {
@@ -69,8 +79,12 @@ struct ecg_ctx {
     int curve = -1;
     int layout = -1;
     void* dev = nullptr;
+    uint64_t fingerprint = 0;  // sampled host records at upload time
   };
   std::vector<BaseCache> base_cache;
+  // MSM terms per device pass (SingleMultiexpKernel::n, multiexp.rs:71-93);
+  // 0 = derived from device memory (msm_chunk_terms)
+  size_t msm_chunk = 0;
   // RCCL communicator of this rank (comm.cpp); size 1 / null = single GPU
   void* comm = nullptr;
   int comm_size = 1;
@@ -130,6 +144,7 @@ int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_base
                   int scalar_mont, size_t line_len, size_t n_chunks, uint32_t window_bits, uint64_t* out_jac,
                   hipStream_t s);
 int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac);
+int msm_pass_terms_run(const ecg_ctx* ctx, int curve_id, size_t* out);
 int gen_bases_run(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n,
                   void* d_out, hipStream_t s);
 

@@ -9,6 +9,9 @@
 //                     + multiexp's device fold          (src/multiexp.rs:394-397)
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include <atomic>
 #include <cstring>
 #include <mutex>
@@ -211,7 +214,7 @@ void ecg_ctx_destroy(ecg_ctx* ctx) {
 }
 
 int ecg_ctx_synchronize(ecg_ctx* ctx) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   ECG_HIP(hipStreamSynchronize(ctx->stream));
   ECG_HIP(hipDeviceSynchronize());
   return ECG_OK;
@@ -229,7 +232,7 @@ int ecg_ctx_info(ecg_ctx* ctx, size_t* mem_bytes, int* compute_units) {
 
 // ---------------------------------------------------------------- FFT
 int ecg_fft_dev(ecg_ctx* ctx, int field_id, void* d_inout, const uint64_t* omega, uint32_t log_n, void* stream) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!d_inout || !omega) {
     set_error("ecg_fft_dev: null pointer");
     return ECG_ERR_INVALID;
@@ -242,7 +245,7 @@ int ecg_fft_dev(ecg_ctx* ctx, int field_id, void* d_inout, const uint64_t* omega
 
 int ecg_fft(ecg_ctx* ctx, int field_id, uint64_t* inout, const uint64_t* omega, uint32_t log_n,
             ecg_abort_cb abort_cb, void* user) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!inout || !omega) {
     set_error("ecg_fft: null pointer");
     return ECG_ERR_INVALID;
@@ -300,7 +303,7 @@ int ecg_fft_many(ecg_ctx** ctxs, int nctx, int field_id, uint64_t** inouts, cons
 // ---------------------------------------------------------------- EC-FFT
 int ecg_ec_fft(ecg_ctx* ctx, int curve_id, uint64_t* inout_jac, const uint64_t* omega, uint32_t log_n,
                ecg_abort_cb abort_cb, void* user) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!inout_jac || !omega) {
     set_error("ecg_ec_fft: null pointer");
     return ECG_ERR_INVALID;
@@ -323,7 +326,7 @@ int ecg_ec_fft(ecg_ctx* ctx, int curve_id, uint64_t* inout_jac, const uint64_t* 
 
 int ecg_ec_fft_dev(ecg_ctx* ctx, int curve_id, void* d_inout_jac, const uint64_t* omega, uint32_t log_n,
                    void* stream) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!d_inout_jac || !omega) {
     set_error("ecg_ec_fft_dev: null pointer");
     return ECG_ERR_INVALID;
@@ -371,7 +374,7 @@ int ecg_ec_fft_many(ecg_ctx** ctxs, int nctx, int curve_id, uint64_t** inouts, c
 // ---------------------------------------------------------------- MSM
 static int msm_host(ecg_ctx* ctx, int curve_id, const uint64_t* bases_xy, const uint64_t* scalars, size_t n,
                     uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if ((!bases_xy || !scalars) && n) {
     set_error("ecg_msm: null pointer");
     return ECG_ERR_INVALID;
@@ -407,7 +410,7 @@ int ecg_msm(ecg_ctx* ctx, int curve_id, const uint64_t* bases_xy, const uint64_t
 
 int ecg_msm_dev(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, void* out_jac,
                 int out_on_device, void* stream) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!out_jac || ((!d_bases || !d_scalars) && n)) {
     set_error("ecg_msm_dev: null pointer");
     return ECG_ERR_INVALID;
@@ -432,7 +435,7 @@ int ecg_msm_dev(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_s
 int ecg_multiple_multiexp(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const uint64_t* scalars,
                           int scalars_on_device, int scalars_montgomery, size_t line_len, size_t num_chunks,
                           uint32_t window_bits, uint64_t* out_jac) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!out_jac || (n_bases && (!d_bases || !scalars))) {
     set_error("ecg_multiple_multiexp: null pointer");
     return ECG_ERR_INVALID;
@@ -465,6 +468,22 @@ void ecg_base_cache_clear(ecg_ctx* ctx) {
   base_cache_free(ctx);
 }
 
+// FNV-1a over up to 16 evenly spaced host records (first and last included):
+// a cache hit must also match the content the entry was uploaded from, so a
+// different array that reuses a freed array's address is not served stale
+// bases (the caller must still not mutate a cached array in place).
+static uint64_t bases_fingerprint(const void* host, size_t n, size_t rec_bytes) {
+  uint64_t h = 1469598103934665603ull ^ n;
+  if (!n) return h;
+  const size_t samples = n < 16 ? n : 16;
+  for (size_t k = 0; k < samples; k++) {
+    const size_t i = samples == 1 ? 0 : k * (n - 1) / (samples - 1);
+    const uint8_t* r = (const uint8_t*)host + i * rec_bytes;
+    for (size_t b = 0; b < rec_bytes; b++) h = (h ^ r[b]) * 1099511628211ull;
+  }
+  return h;
+}
+
 // Bases [x, y] on the device for (bases, layout, n): from the cache, or
 // uploaded (and converted from the ark layout) into `slot`.
 static int stage_bases(ecg_ctx* ctx, int curve_id, const void* bases, int layout, size_t n, int cache,
@@ -473,12 +492,23 @@ static int stage_bases(ecg_ctx* ctx, int curve_id, const void* bases, int layout
   const size_t xy_bytes = n * 2 * lq * 8;
   const size_t raw_bytes = layout == ECG_BASES_ARK_AFFINE ? n * (2 * lq + 1) * 8 : xy_bytes;
   hipStream_t s = ctx->stream;
+  const size_t rec = layout == ECG_BASES_ARK_AFFINE ? (2 * lq + 1) * 8 : 2 * lq * 8;
+  uint64_t fp = 0;
   if (cache) {
-    for (auto& e : ctx->base_cache)
+    fp = bases_fingerprint(bases, n, rec);
+    for (size_t k = 0; k < ctx->base_cache.size(); k++) {
+      auto& e = ctx->base_cache[k];
       if (e.host == bases && e.n == n && e.curve == curve_id && e.layout == layout) {
-        *d_xy = e.dev;
-        return ECG_OK;
+        if (e.fingerprint == fp) {
+          *d_xy = e.dev;
+          return ECG_OK;
+        }
+        ECG_HIP(hipStreamSynchronize(s));  // same address, other content: drop the stale entry
+        (void)hipFree(e.dev);
+        ctx->base_cache.erase(ctx->base_cache.begin() + k);
+        break;
       }
+    }
   }
   void* dst;
   if (cache) {
@@ -507,7 +537,7 @@ static int stage_bases(ecg_ctx* ctx, int curve_id, const void* bases, int layout
       (void)hipFree(ctx->base_cache.front().dev);
       ctx->base_cache.erase(ctx->base_cache.begin());
     }
-    ctx->base_cache.push_back({bases, n, curve_id, layout, dst});
+    ctx->base_cache.push_back({bases, n, curve_id, layout, dst, fp});
   }
   *d_xy = dst;
   return ECG_OK;
@@ -516,7 +546,7 @@ static int stage_bases(ecg_ctx* ctx, int curve_id, const void* bases, int layout
 int ecg_msm_ex(ecg_ctx* ctx, int curve_id, const void* bases, int bases_layout, size_t n_bases, size_t skip,
                const uint64_t* exps, int exps_montgomery, size_t n_exps, const uint64_t* density, int cache_bases,
                uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!out_jac || (n_exps && !exps) || (n_bases && !bases)) {
     set_error("ecg_msm_ex: null pointer");
     return ECG_ERR_INVALID;
@@ -569,7 +599,7 @@ int ecg_msm_ex(ecg_ctx* ctx, int curve_id, const void* bases, int bases_layout, 
 
 int ecg_point_sum_dev(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count, uint64_t* out_jac,
                       void* stream) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!out_jac || (!d_points && count)) {
     set_error("ecg_point_sum_dev: null pointer");
     return ECG_ERR_INVALID;
@@ -579,7 +609,7 @@ int ecg_point_sum_dev(ecg_ctx* ctx, int curve_id, const void* d_points, size_t c
 
 // ---------------------------------------------------------------- device buffers
 int ecg_dev_alloc(ecg_ctx* ctx, size_t bytes, void** out) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!out) {
     set_error("ecg_dev_alloc: null out pointer");
     return ECG_ERR_INVALID;
@@ -602,14 +632,14 @@ void ecg_dev_free(ecg_ctx* ctx, void* p) {
 }
 
 int ecg_dev_upload(ecg_ctx* ctx, void* d_dst, const void* src, size_t bytes) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   ECG_HIP(hipMemcpyAsync(d_dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
   ECG_HIP(hipStreamSynchronize(ctx->stream));
   return ECG_OK;
 }
 
 int ecg_dev_download(ecg_ctx* ctx, void* dst, const void* d_src, size_t bytes) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   ECG_HIP(hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   ECG_HIP(hipStreamSynchronize(ctx->stream));
   return ECG_OK;
@@ -687,12 +717,49 @@ int ecg_msm_check_bases(int curve_id, const uint64_t* bases_xy, const uint64_t* 
 
 int ecg_gen_bases_dev(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n, void* d_out,
                       void* stream) {
-  ECG_TRY(ctx_enter(ctx));
+  ECG_ENTER(ctx);
   if (!a || !b || (!d_out && n)) {
     set_error("ecg_gen_bases_dev: null pointer");
     return ECG_ERR_INVALID;
   }
   return gen_bases_run(ctx, curve_id, a, b, n, d_out, pick_stream(ctx, stream));
+}
+
+int ecg_ctx_set_msm_chunk(ecg_ctx* ctx, size_t max_terms) {
+  ECG_ENTER(ctx);
+  if (max_terms > 0x7fffffffull) {
+    set_error("ecg_ctx_set_msm_chunk: at most 2^31-1 terms per pass");
+    return ECG_ERR_INVALID;
+  }
+  ctx->msm_chunk = max_terms;
+  return ECG_OK;
+}
+
+int ecg_msm_chunk_size(ecg_ctx* ctx, int curve_id, size_t* out) {
+  ECG_ENTER(ctx);
+  if (!out) {
+    set_error("ecg_msm_chunk_size: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  return msm_pass_terms_run(ctx, curve_id, out);
+}
+
+const char* ecg_runtime_info(void) {
+  static std::string info;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    int hv = 0, nv = 0;
+    (void)hipRuntimeGetVersion(&hv);
+    (void)ncclGetVersion(&nv);
+    Dl_info dh{}, dn{};
+    (void)dladdr(reinterpret_cast<void*>(&hipRuntimeGetVersion), &dh);
+    (void)dladdr(reinterpret_cast<void*>(&ncclGetVersion), &dn);
+    char buf[1024];
+    snprintf(buf, sizeof buf, "hip=%d (%s); rccl=%d (%s)", hv, dh.dli_fname ? dh.dli_fname : "?", nv,
+             dn.dli_fname ? dn.dli_fname : "?");
+    info = buf;
+  });
+  return info.c_str();
 }
 
 int ecg_last_kernel_time(ecg_ctx* ctx, const char* name, double* ms_total, int* launches) {

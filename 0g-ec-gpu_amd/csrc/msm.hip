@@ -82,6 +82,13 @@ int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count
   return point_sum_host(curve_id, pts.data(), count, out_jac);
 }
 
+int msm_pass_terms_run(const ecg_ctx* ctx, int curve_id, size_t* out) {
+  const MsmOps* o = msm_ops(curve_id, "multiexp");
+  if (!o) return ECG_ERR_INVALID;
+  *out = o->pass_terms(ctx);
+  return ECG_OK;
+}
+
 int gen_bases_run(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n, void* d_out,
                   hipStream_t s) {
   const MsmOps* o = msm_ops(curve_id, "gen_bases");

@@ -59,7 +59,7 @@ namespace ecg {
 
 constexpr int MSM_THREADS = 256;
 constexpr uint32_t MSM_FOLD = 32;        // fan-in of the partial-sum tree
-constexpr size_t MSM_MAX_CHUNK = 1ull << 27;  // terms per device pass
+constexpr double MSM_MEMORY_PADDING = 0.2;    // share of HBM left free (multiexp.rs:24)
 constexpr uint32_t MSM_COMBINE_SEG = 32;      // records per thread in msm_combine
 
 // Tunables (env overrides for A/B measurement in one build).
@@ -849,8 +849,36 @@ int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const M
   return msm_core_impl<C, typename C::Fq>(ctx, d_bases, d_scalars, g, pl, s, d_sums);
 }
 
-// One MSM, processed in device passes of at most MSM_MAX_CHUNK terms; the
-// window sums come back to the host, which runs the Horner fold.
+// Terms per device pass: calc_chunk_size (multiexp.rs:71-93) restated for
+// this pipeline's workspace.  Per term: the staged input base
+// and scalar (host-slice entry points), the reduced-radix base record, W
+// double-buffered (key, value) pairs and the segment-edge records (2 per SEG
+// entries, + 1/16 for the next combine level); fixed: the W x B buckets and
+// the sort's scratch.  MEMORY_PADDING of the device memory and the resident
+// base cache are left alone.  ecg_ctx_set_msm_chunk pins the value instead.
+template <class C>
+size_t msm_pass_terms(const ecg_ctx* ctx) {
+  if (ctx->msm_chunk) return ctx->msm_chunk;
+  using F = typename C::Fq;
+  constexpr bool rr = has_rr_form<C>();
+  using AF = std::conditional_t<rr, FpR<typename RRof<typename C::FqParams>::Q>, F>;
+  const MsmPlan pl = make_plan((size_t)1 << 26, (uint32_t)C::FrParams::BITS);
+  const double per_term = 2.0 * sizeof(F) + 32.0 + (rr ? (double)BaseLayout<AF>::BYTES : 0.0) + 16.0 * pl.W +
+                          2.0 * pl.W / pl.seg * (sizeof(XYZZ<AF>) + 4) * (1.0 + 1.0 / 16);
+  const double fixed = (double)pl.W * pl.B * sizeof(XYZZ<AF>) + 256.0 * (1 << 20);
+  double cached = 0;
+  for (const auto& e : ctx->base_cache) cached += (double)e.n * 2 * sizeof(F);
+  const double budget = (double)ctx->mem_bytes * (1.0 - MSM_MEMORY_PADDING) - cached - fixed;
+  double t = budget / per_term;
+  if (!(t >= (double)(1u << 16))) t = (double)(1u << 16);  // tiny / unknown memory: still make progress
+  if (t > (double)0x7fffffffu) t = (double)0x7fffffffu;   // 31-bit term indices
+  return (size_t)t;
+}
+
+// One MSM, processed in device passes of msm_pass_terms terms (the
+// reference's sub-chunk loop, multiexp.rs:348-361, with the abort poll before
+// each pass, :140-144); the window sums come back to the host, which runs the
+// Horner fold of each pass and adds the passes up.
 template <class C>
 int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
                         hipStream_t s, ecg_abort_cb abort_cb, void* user, uint32_t scalar_mont) {
@@ -860,9 +888,10 @@ int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_
   kt_reset(ctx, "msm_accumulate");
   HX total_acc = HX::zero();
   std::vector<X> win;
-  for (size_t off = 0; off < n; off += MSM_MAX_CHUNK) {
+  const size_t chunk = msm_pass_terms<C>(ctx);
+  for (size_t off = 0; off < n; off += chunk) {
     if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144
-    const size_t m = n - off < MSM_MAX_CHUNK ? n - off : MSM_MAX_CHUNK;
+    const size_t m = n - off < chunk ? n - off : chunk;
     const MsmPlan pl = make_plan(m, (uint32_t)C::FrParams::BITS);
     const MsmGeom g{1, 1, m, m, scalar_mont};
     void* d_sums;

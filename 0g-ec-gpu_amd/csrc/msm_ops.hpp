@@ -11,6 +11,7 @@ struct MsmOps {
                size_t line_len, uint32_t scalar_mont, uint32_t window_bits, uint64_t* out_jac, hipStream_t);
   int (*point_sum)(const uint64_t* points, size_t count, uint64_t* out_jac);
   int (*gen_bases)(ecg_ctx*, const uint64_t* a, const uint64_t* b, size_t n, void* d_out, hipStream_t);
+  size_t (*pass_terms)(const ecg_ctx*);
 };
 
 }  // namespace ecg

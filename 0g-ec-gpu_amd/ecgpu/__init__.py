@@ -103,6 +103,9 @@ _SIGS = {
                                   ABORT_CB, ctypes.c_void_p]),
     "ecg_base_cache_clear": (None, [ctypes.c_void_p]),
     "ecg_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "ecg_msm_chunk_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    "ecg_ctx_set_msm_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "ecg_runtime_info": (ctypes.c_char_p, []),
     "ecg_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "ecg_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "ecg_comm_destroy": (None, [ctypes.c_void_p]),
@@ -289,6 +292,17 @@ class Program:
 
     def synchronize(self) -> None:
         _check(lib().ecg_ctx_synchronize(self.handle), "synchronize")
+
+    def msm_chunk_size(self, curve="bls12_381") -> int:
+        """Terms per MSM device pass (SingleMultiexpKernel::n / calc_chunk_size,
+        multiexp.rs:71-93), derived from this device's memory unless pinned."""
+        n = ctypes.c_size_t()
+        _check(lib().ecg_msm_chunk_size(self.handle, _curve(curve), ctypes.byref(n)), "msm_chunk_size")
+        return n.value
+
+    def set_msm_chunk(self, max_terms: int) -> None:
+        """Pin the terms per MSM device pass (0 = derived from device memory)."""
+        _check(lib().ecg_ctx_set_msm_chunk(self.handle, int(max_terms)), "set_msm_chunk")
 
     def kernel_time(self, name: str) -> tuple[float, int]:
         ms = ctypes.c_double()
@@ -696,6 +710,15 @@ class DensityTracker:
         bits[:m] = np.asarray(self.bv[:m], dtype=np.uint8)
         return np.ascontiguousarray(np.packbits(bits, bitorder="little").view(np.uint64))
 
+    def clone(self) -> "DensityTracker":
+        d = DensityTracker(self.bv)
+        d.total_density = self.total_density
+        return d
+
+    def __eq__(self, other) -> bool:  # #[derive(PartialEq)]: bv and total_density
+        return isinstance(other, DensityTracker) and self.bv == other.bv and \
+            self.total_density == other.total_density
+
     def generate_exps(self, exponents: np.ndarray) -> np.ndarray:
         keep = np.asarray(self.bv[:len(exponents)], dtype=bool)
         return exponents[:len(keep)][keep]
@@ -706,7 +729,12 @@ class SingleMultiexpKernel:
         self.program = prog
         self.cid = cid
         self.maybe_abort = maybe_abort
-        self.n = 1 << 31  # terms per call the device handles (calc_chunk_size analogue)
+
+    @property
+    def n(self) -> int:
+        """Terms per device pass (multiexp.rs:61-63 `n`, from calc_chunk_size);
+        longer inputs run as several passes inside one call."""
+        return self.program.msm_chunk_size(self.cid)
 
     def multiexp(self, bases: np.ndarray, exps: np.ndarray) -> np.ndarray:
         lq = CURVE_FQ_LIMBS[self.cid]
@@ -777,6 +805,14 @@ class MultiexpKernel:
         lq = CURVE_FQ_LIMBS[cid]
         rec = 2 * lq + 1 if ark_affine else 2 * lq
         b = np.ascontiguousarray(bases, dtype=np.uint64).reshape(-1, rec)
+        if cache_bases:
+            # the cache is keyed by the host address: cache only the caller's
+            # own array (never a temporary copy), and keep it alive while cached
+            if not isinstance(bases, np.ndarray) or not np.shares_memory(b, bases):
+                raise EcError("multiexp_ex(cache_bases=True) needs a C-contiguous uint64 bases array "
+                              "(a converted copy cannot be cached by address)")
+            pins = k.program.__dict__.setdefault("_base_pins", {})
+            pins[b.ctypes.data] = bases
         e = np.ascontiguousarray(exps, dtype=np.uint64).reshape(-1, 4)
         dens = None
         if density is not None and not isinstance(density, FullDensity):
@@ -794,6 +830,7 @@ class MultiexpKernel:
     def clear_base_cache(self) -> None:
         for k in self.kernels:
             lib().ecg_base_cache_clear(k.program.handle)
+            k.program.__dict__.pop("_base_pins", None)
 
 
 def check_bases(curve, bases: np.ndarray, exps: np.ndarray) -> None:

@@ -15,14 +15,106 @@ assigned by chunk; nothing is exchanged.  One transform too large for a GPU,
 or already block-distributed, runs as ecg_fft_dist (three RCCL all-to-alls,
 dfft.hip).
 
-RCCL lives inside libecgpu (same HIP runtime as its device buffers);
-torch.distributed (any backend, gloo on CPU is enough) only carries the
-128-byte rendezvous id (comm_init).  msm_sharded keeps the orchestration
-injectable so the CPU multi-process tests (gloo) exercise the same split.
+RCCL lives inside libecgpu, on the ROCm install's HIP runtime (the same one
+as its device buffers).  The host side of a launch -- the 128-byte RCCL id,
+barriers, the max over ranks of a timing -- needs only a few small messages:
+HostGroup carries them over one local TCP socket per rank, so a launched
+process never loads a second HIP runtime (torch bundles its own copies of
+libamdhip64 / librccl; importing it next to libecgpu maps both).  Any group
+with a broadcast works for comm_init (torch.distributed in the gloo tests).
+msm_sharded keeps the orchestration injectable so the CPU multi-process tests
+exercise the same split.
 """
 from __future__ import annotations
 
-from typing import Callable, Sequence
+import os
+import time
+from typing import Any, Callable, Sequence
+
+
+class HostGroup:
+    """Rank 0 listens on (addr, port); every other rank connects.  Collectives
+    are star-shaped through rank 0 (small host objects only: ids, timings,
+    digests).  From a torch.distributed.run launch: HostGroup.from_env()."""
+
+    def __init__(self, rank: int, world: int, addr: str = "127.0.0.1", port: int = 29600,
+                 authkey: bytes = b"ecgpu-hostgroup", timeout: float = 300.0):
+        from multiprocessing.connection import Client, Listener
+
+        if world <= 0 or not (0 <= rank < world):
+            raise ValueError("bad world/rank")
+        self.rank, self.world = rank, world
+        self._peers = []
+        self._conn = None
+        self._listener = None
+        if world == 1:
+            return
+        if rank == 0:
+            self._listener = Listener((addr, port), authkey=authkey)
+            peers = {}
+            while len(peers) < world - 1:
+                c = self._listener.accept()
+                r = c.recv()
+                peers[r] = c
+            self._peers = [peers[r] for r in range(1, world)]
+        else:
+            deadline = time.time() + timeout
+            while True:
+                try:
+                    self._conn = Client((addr, port), authkey=authkey)
+                    break
+                except (ConnectionRefusedError, FileNotFoundError, OSError):
+                    if time.time() > deadline:
+                        raise
+                    time.sleep(0.05)
+            self._conn.send(rank)
+
+    @staticmethod
+    def from_env(offset: int = 1) -> "HostGroup":
+        """RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT as torch.distributed.run
+        sets them; the group listens on MASTER_PORT + offset (the launcher's
+        own store holds MASTER_PORT)."""
+        rank = int(os.environ.get("RANK", "0"))
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = int(os.environ.get("MASTER_PORT", "29500")) + offset
+        return HostGroup(rank, world, addr, port)
+
+    def allgather(self, obj: Any) -> list:
+        if self.world == 1:
+            return [obj]
+        if self.rank == 0:
+            out = [obj] + [c.recv() for c in self._peers]
+            for c in self._peers:
+                c.send(out)
+            return out
+        self._conn.send(obj)
+        return self._conn.recv()
+
+    def broadcast(self, obj: Any = None) -> Any:
+        """rank 0's obj on every rank."""
+        if self.world == 1:
+            return obj
+        if self.rank == 0:
+            for c in self._peers:
+                c.send(obj)
+            return obj
+        return self._conn.recv()
+
+    def barrier(self) -> None:
+        self.allgather(None)
+
+    def max(self, x: float) -> float:
+        return max(self.allgather(float(x)))
+
+    def close(self) -> None:
+        for c in self._peers:
+            c.close()
+        if self._conn is not None:
+            self._conn.close()
+        if self._listener is not None:
+            self._listener.close()
+        self._peers, self._conn, self._listener = [], None, None
 
 
 def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
@@ -68,24 +160,53 @@ def msm_sharded(n: int, partial_fn: Callable[[int, int], "object"], fold_fn: Cal
 # ---------------------------------------------------------------------------
 
 
-def comm_init(prog, rank: int, world: int, dist_mod=None, group=None) -> None:
-    """Rank 0 makes the RCCL id, the launcher's process group broadcasts it,
-    every rank binds its Program's context (ecg_comm_init)."""
+def comm_init(prog, rank: int, world: int, broadcast: Callable[[Any], Any] | None = None,
+              make_id: Callable[[], bytes] | None = None) -> None:
+    """Rank 0 makes the RCCL id (make_id, default ecg_comm_unique_id), the
+    launcher's group broadcasts it (broadcast(obj) -> rank 0's obj, e.g.
+    HostGroup.broadcast), every rank binds its Program's context
+    (ecg_comm_init).  make_id is injectable so the CPU tests run the same
+    exchange without RCCL."""
     import ctypes
 
     import ecgpu
 
     buf = (ctypes.c_uint8 * 128)()
     if world > 1:
-        if dist_mod is None:
-            import torch.distributed as dist_mod
-        obj = [None]
+        ident = None
         if rank == 0:
-            ecgpu._check(ecgpu.lib().ecg_comm_unique_id(buf), "comm_unique_id")
-            obj = [bytes(buf)]
-        dist_mod.broadcast_object_list(obj, src=0, group=group)
-        ctypes.memmove(buf, obj[0], 128)
+            ident = make_id() if make_id is not None else unique_id()
+        ident = broadcast(ident)
+        if not isinstance(ident, (bytes, bytearray)) or len(ident) != 128:
+            raise ValueError("comm_init: the broadcast RCCL id must be 128 bytes")
+        ctypes.memmove(buf, bytes(ident), 128)
+    if prog is None:  # exchange only (CPU tests)
+        return bytes(buf)
     ecgpu._check(ecgpu.lib().ecg_comm_init(prog.handle, world, rank, buf), "comm_init")
+    return bytes(buf)
+
+
+def unique_id() -> bytes:
+    import ctypes
+
+    import ecgpu
+
+    buf = (ctypes.c_uint8 * 128)()
+    ecgpu._check(ecgpu.lib().ecg_comm_unique_id(buf), "comm_unique_id")
+    return bytes(buf)
+
+
+def torch_broadcast(dist_mod=None, group=None) -> Callable[[Any], Any]:
+    """broadcast(obj) over a torch.distributed group (gloo tests)."""
+    if dist_mod is None:
+        import torch.distributed as dist_mod
+
+    def bcast(obj):
+        lst = [obj]
+        dist_mod.broadcast_object_list(lst, src=0, group=group)
+        return lst[0]
+
+    return bcast
 
 
 def msm_dist(prog, curve, d_bases, d_scalars, n_local: int):

@@ -3,22 +3,29 @@
 
 Workload (BASELINE.json metric): one step = one G1 Pippenger MSM over 2^26
 (base, scalar) terms.  The terms are sharded in contiguous ranges across the N
-ranks (BASELINE config 4; at N=1 the whole 2^26 runs on one GPU).  The per-rank
-partial sums are all-gathered over RCCL (linked into libecgpu, ecg_msm_dist)
-and folded; torch.distributed (gloo, CPU) only does the rendezvous, barriers
-and the max-over-ranks of the step time -- torch never touches the GPU.
-The NTT leg times one in-place 2^24 Fr NTT per rank per step (radix_fft_many
-semantics: whole transforms per GPU, no exchange); it is reported in "ntt".
+ranks (BASELINE config 4, multiexp.rs:332-336; at N=1 the whole 2^26 runs on
+one GPU).  The per-rank partial sums are all-gathered over RCCL (linked into
+libecgpu, ecg_msm_dist) and folded.  The host side of the launch (RCCL id,
+barriers, max over ranks) runs over ecgpu.dist.HostGroup: this process never
+imports torch, so the only HIP runtime and RCCL in it are the ROCm install's
+(checked at start-up, ecg_runtime_info).
+
+NTT legs: one in-place 2^24 Fr NTT per rank per step (radix_fft_many
+semantics: whole transforms per GPU, no exchange; "ntt"), and at N > 1 one
+2^24 NTT block-distributed over the N ranks (ecg_fft_dist, three RCCL
+all-to-alls; "ntt_dist").
 
 Inputs are synthetic and resident in HBM (library-owned device buffers)
 before the timed region: bases P_i = (a + i*b) G generated on the GPU,
-scalars uniform < r (seeded numpy), NTT input uniform Fr.
+scalars uniform < r (seeded numpy, one stream per rank), NTT input uniform Fr.
 value = total MSM terms / step time (whole job, max over ranks).
 
-At N=1 the oracle leg (CPU, rank 0) checks the MSM result against the
-known answer (sum s_i (a + i b) mod r) G at the full 2^26, checks the NTT
-bit-exactly against the CPU parallel_fft at the full 2^24, and times the CPU
-restatements as the baseline.
+Checks, at every N, on rank 0 with the CPU oracle (the checker only):
+the MSM result against the known answer (sum_j s_j (a + j b) mod r) G over all
+2^26 terms (rank 0 regenerates every rank's scalars), the single-GPU NTT
+bit-exactly against the CPU parallel_fft, and at N > 1 every rank's block of
+the distributed NTT (SHA-256 digests) against the same parallel_fft.  Rank 0
+at N=1 also times the CPU restatements as the baseline.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under
 torch.distributed.run (one process per GPU).
@@ -26,6 +33,7 @@ torch.distributed.run (one process per GPU).
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -36,8 +44,12 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "0g-ec-gpu_amd"))
 import ecgpu  # noqa: E402  (product path: libecgpu.so, fails loudly if missing)
+from ecgpu import dist as edist  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s
+# v_mad_u64_u32 issue peak: 256 CUs x 4 SIMDs x 16 lanes per cycle (one wave64
+# VALU instruction per 4 cycles per SIMD) at the 2.4 GHz peak clock
+MAD_PEAK_T = 256 * 4 * 16 * 2.4e9 / 1e12
 R_BLS = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 R_BN = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
 P_BLS = int("1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab", 16)
@@ -46,15 +58,19 @@ MSM_SEED = 0x35A00026
 NTT_SEED = 0x0FF70024
 KAT_A = 0x1234567890ABCDEF1122334455667788
 KAT_B = 0x0FEDCBA987654321
-# VALU roofs (the kernels are VALU-bound; AMD publishes no integer-MAD rate, so
-# these are measured field-product rates on MI355X):
-#  * MSM accumulation: 10 Fq products per term per window (madd-2008-s, 8M+2S)
-#    in the reduced-radix form; roof = the 8M+2S mix of the paired product /
-#    squaring rates (tools/rr_bench.hip, profiles/r01d/rr_bench.log).
-#  * NTT: exact Fr products per transform (ntt_fr_muls) vs the 32-bit-limb Fr
-#    product rate (tools/field_bench.hip, profiles/r01/field_bench_ilp2.log).
-FQ_MIX_PEAK_G = {0: 10 / (8 / 76.89 + 2 / 93.95), 1: 10 / (8 / 144.55 + 2 / 172.14)}
-FR_MUL_PEAK_G = 132.65
+# reduced-radix limbs of the MSM's Fq (fieldrr.hpp): 14 x 29 bits (BLS12-381), 10 x 28 (BN254)
+RR_LIMBS = {0: 14, 1: 10}
+FR_MUL_PEAK_G = 132.65         # measured 32-bit-limb Fr product rate (profiles/r01/field_bench_ilp2.log)
+
+
+def madd_mads(nl: int) -> int:
+    """v_mad_u64_u32 per XYZZ mixed add (rr_add_affine, curve_rr.hpp): three
+    paired products (2 NL^2 each: schoolbook + Montgomery reduction) x 2, one
+    paired squaring (NL(NL+1)/2 + NL^2) x 2, one product sum with a shared
+    reduction (3 NL^2).  3542 for BLS12-381 (matches SQ_INSTS_VALU_INT64 per
+    add, profiles/r02)."""
+    mul, sqr = 2 * nl * nl, nl * (nl + 1) // 2 + nl * nl
+    return 6 * mul + 2 * sqr + 3 * nl * nl
 
 
 def ntt_fr_muls(log_n: int, max_deg: int = 10) -> float:
@@ -79,7 +95,7 @@ def ntt_fr_muls(log_n: int, max_deg: int = 10) -> float:
     return total
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -88,11 +104,25 @@ def parse():
     ap.add_argument("--ntt-log", type=int, default=24)
     ap.add_argument("--curve", default="bls12_381")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--msm-cpu-log", type=int, default=20)
+    ap.add_argument("--no-check", action="store_true", help="skip the oracle checks (profiling runs)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (default: EC_GPU_NUM_THREADS, else OMP_NUM_THREADS, else affinity)")
+    ap.add_argument("--msm-cpu-log", type=int, default=23)
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive API timings (N=1)")
     ap.add_argument("--no-aux", action="store_true", help="skip the batched-MSM / EC-FFT side lines (N=1)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def cpu_threads(arg: int) -> int:
+    """threadpool.rs:25-30: EC_GPU_NUM_THREADS, else every CPU this process may
+    use (OMP_NUM_THREADS on the GPU box names its CPU share)."""
+    if arg > 0:
+        return arg
+    for var in ("EC_GPU_NUM_THREADS", "OMP_NUM_THREADS"):
+        v = os.environ.get(var, "")
+        if v.isdigit() and int(v) > 0:
+            return int(v)
+    return len(os.sched_getaffinity(0))
 
 
 def u64(x: int, n: int = 4) -> np.ndarray:
@@ -122,25 +152,38 @@ def rand_scalars(rng: np.random.Generator, n: int, r: int) -> np.ndarray:
     return out
 
 
-def pmc_traffic(kernel: str, streaming_read: bool):
-    """HBM bytes per launch (GB) from the committed rocprofv3 PMC passes
-    (tools/gpu_prof.sh -> profiles/<round>/pmc_fetch_write.json): FETCH_SIZE +
-    WRITE_SIZE.  gfx950 FETCH_SIZE counts half the bytes of wide coalesced
-    streaming reads (MI355X_MICROARCH.md, HBM/rocprofv3 section), so those are
-    doubled; gathers are reported as counted."""
-    import glob
+def msm_shard(rank: int, world: int, n_total: int, r_int: int):
+    """This rank's MSM shard: contiguous range (multiexp.rs:332-336), its
+    scalars (seed stream [MSM_SEED, rank]) and the base generator offset:
+    P_{i0 + i} = (KAT_A + (i0 + i) KAT_B) G = (a_loc + i KAT_B) G."""
+    i0, i1 = edist.shard_range(n_total, world, rank)
+    scal = rand_scalars(np.random.default_rng([MSM_SEED, rank]), i1 - i0, r_int)
+    return i0, i1 - i0, scal, (KAT_A + i0 * KAT_B) % r_int
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_fetch_write.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    for k, v in d.items():
-        if kernel in k:
-            fetch = v["FETCH_SIZE"]["mean_kb"] * 1024 / 1e9
-            write = v["WRITE_SIZE"]["mean_kb"] * 1024 / 1e9
-            return (2 * fetch if streaming_read else fetch) + write, os.path.relpath(files[-1], ROOT)
-    return None, None
+
+def msm_kat_scalar(co, cid: int, world: int, n_total: int, r_int: int, nthreads: int, shards=None) -> int:
+    """sum_j s_j (KAT_A + j KAT_B) mod r over every rank's shard (regenerated
+    from the per-rank seeds unless `shards` hands them in)."""
+    k = 0
+    for r in range(world):
+        _, n_loc, scal, a_loc = shards[r] if shards is not None else msm_shard(r, world, n_total, r_int)
+        if n_loc:
+            k = (k + co.kat_scalar(cid, a_loc, KAT_B, scal, nthreads=nthreads)) % r_int
+    return k
+
+
+def omega_for(cid: int, r_int: int, ln: int) -> np.ndarray:
+    """TWO_ADIC_ROOT^(2^(S - log n)) in Montgomery form (tests/fft.rs:16-24)."""
+    gen, two_adicity = (7, 32) if cid == 0 else (5, 28)
+    w = pow(gen, (r_int - 1) >> two_adicity, r_int)
+    for _ in range(ln, two_adicity):
+        w = w * w % r_int
+    return u64(w * (1 << 256) % r_int)
+
+
+def block_digests(a: np.ndarray, world: int) -> list:
+    m = a.shape[0] // world
+    return [hashlib.sha256(np.ascontiguousarray(a[r * m:(r + 1) * m]).tobytes()).hexdigest() for r in range(world)]
 
 
 def main():
@@ -148,61 +191,46 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = torch = None
-    if world > 1:
-        # Rendezvous only (CPU / gloo): the device exchange is RCCL inside
-        # libecgpu, on the same HIP runtime as its buffers.
-        import torch
-        import torch.distributed as dist
+    if world != args.gpus and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
 
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo")
+    # the library (and through it the ROCm install's HIP runtime and RCCL) is
+    # the first GPU code this process loads; torch is never imported
+    runtime = ecgpu.lib().ecg_runtime_info().decode()
+    if "/opt/rocm" not in runtime:
+        raise SystemExit(f"libecgpu bound a foreign HIP runtime / RCCL: {runtime}")
+    if rank == 0:
+        print(f"runtime: {runtime}", file=sys.stderr)
 
+    group = edist.HostGroup.from_env() if world > 1 else edist.HostGroup(0, 1)
     cid = ecgpu.CURVE_NAMES[args.curve]
     fr_fid = ecgpu.CURVE_FR_FIELD[cid]
     lq = ecgpu.CURVE_FQ_LIMBS[cid]
     r_int = R_BLS if cid == 0 else R_BN
     prog = ecgpu.program(ecgpu.Device(local_rank))
     if world > 1:
-        from ecgpu import dist as edist
-
-        edist.comm_init(prog, rank, world, dist)
+        edist.comm_init(prog, rank, world, group.broadcast)
+    nthreads = cpu_threads(args.cpu_threads)
 
     # ------------------------------------------------------------ MSM inputs (HBM-resident)
     n_total = 1 << args.msm_log
-    per = (n_total + world - 1) // world
-    i0 = min(n_total, rank * per)
-    n_loc = min(n_total, i0 + per) - i0
-    rng = np.random.default_rng([MSM_SEED, rank])
-    scal = rand_scalars(rng, n_loc, r_int)
+    i0, n_loc, scal, a_loc = msm_shard(rank, world, n_total, r_int)
     d_scal = ecgpu.DeviceBuffer.upload(prog, scal)
-    a_loc = (KAT_A + i0 * KAT_B) % r_int
     d_bases = ecgpu.gen_bases_dev(prog, args.curve, a_loc, KAT_B, n_loc)
     result = np.zeros(3 * lq, dtype=np.uint64)
 
     def msm_step():
         if world == 1:
             result[:] = ecgpu.msm_dev(prog, args.curve, d_bases, d_scal, n_loc)
-            return
-        # local MSM + RCCL all-gather of world x 144 B partials + fold (no EC-add reduce op in RCCL)
-        result[:] = edist.msm_dist(prog, args.curve, d_bases, d_scal, n_loc)
+        else:  # local MSM + RCCL all-gather of world x 144 B partials + fold (no EC-add reduce op in RCCL)
+            result[:] = edist.msm_dist(prog, args.curve, d_bases, d_scal, n_loc)
 
     # ------------------------------------------------------------ NTT inputs (HBM-resident)
     log_n = args.ntt_log
     n_ntt = 1 << log_n
-    # omega = TWO_ADIC_ROOT^(2^(S - log n)) (ec-gpu-proxy/tests/fft.rs:16-24); Montgomery R = 2^256
-    gen, two_adicity = (7, 32) if cid == 0 else (5, 28)
-    omega = pow(gen, (r_int - 1) >> two_adicity, r_int)
-    for _ in range(log_n, two_adicity):
-        omega = omega * omega % r_int
-    omega_m = u64(omega * (1 << 256) % r_int)
-
-    def omega_for(ln: int) -> np.ndarray:
-        w = pow(gen, (r_int - 1) >> two_adicity, r_int)
-        for _ in range(ln, two_adicity):
-            w = w * w % r_int
-        return u64(w * (1 << 256) % r_int)
-    ntt_in = rand_scalars(np.random.default_rng([NTT_SEED, rank]), n_ntt, r_int)  # any value < r is a Montgomery form
+    omega_m = omega_for(cid, r_int, log_n)
+    # any value < r is a Montgomery form; every rank holds the same seeded input
+    ntt_in = rand_scalars(np.random.default_rng([NTT_SEED, 0]), n_ntt, r_int)
     d_ntt = ecgpu.DeviceBuffer.upload(prog, ntt_in)
 
     def ntt_step():
@@ -213,15 +241,7 @@ def main():
         # every libecgpu call returns after its stream is synchronised, so the
         # device is idle here; the barrier lines the ranks up
         prog.synchronize()
-        if world > 1:
-            dist.barrier()
-
-    def max_over_ranks(x: float) -> float:
-        if world == 1:
-            return x
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        group.barrier()
 
     # ------------------------------------------------------------ MSM timing (every call is synchronous)
     for _ in range(args.warmup):
@@ -236,10 +256,11 @@ def main():
         acc_ms += ms
         acc_launch += cnt
     barrier()
-    msm_s = max_over_ranks(time.perf_counter() - t0) / args.steps
-    acc_avg_ms = max_over_ranks(acc_ms / max(acc_launch, 1))
+    msm_s = group.max(time.perf_counter() - t0) / args.steps
+    acc_avg_ms = group.max(acc_ms / max(acc_launch, 1))
+    msm_result = result.copy()
 
-    # ------------------------------------------------------------ NTT timing
+    # ------------------------------------------------------------ NTT timing (one transform per GPU)
     for _ in range(args.warmup):
         ntt_step()
     barrier()
@@ -251,51 +272,82 @@ def main():
         pass_ms += ms
         pass_launch += cnt
     barrier()
-    ntt_s = max_over_ranks(time.perf_counter() - t0) / args.steps
-    pass_avg_ms = max_over_ranks(pass_ms / max(pass_launch, 1))
+    ntt_s = group.max(time.perf_counter() - t0) / args.steps
+    pass_avg_ms = group.max(pass_ms / max(pass_launch, 1))
     passes_per_ntt = pass_launch / args.steps
 
-    # ------------------------------------------------------------ oracle leg (rank 0, N = 1)
+    # ------------------------------------------------------------ distributed NTT (N > 1): one 2^24 over all ranks
+    ntt_dist = None
+    dist_digests = None
+    if world > 1:
+        m = n_ntt // world
+        d_blk = ecgpu.DeviceBuffer.upload(prog, ntt_in[rank * m:(rank + 1) * m])
+        for _ in range(args.warmup):
+            edist.fft_dist(prog, args.curve + "_fr", d_blk, omega_m, log_n)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            edist.fft_dist(prog, args.curve + "_fr", d_blk, omega_m, log_n)
+        barrier()
+        fd_s = group.max(time.perf_counter() - t0) / args.steps
+        # checked run: fresh input block, one transform
+        d_blk.write(ntt_in[rank * m:(rank + 1) * m])
+        edist.fft_dist(prog, args.curve + "_fr", d_blk, omega_m, log_n)
+        blk = d_blk.read(shape=(m, 4))
+        dist_digests = group.allgather(hashlib.sha256(blk.tobytes()).hexdigest())
+        d_blk.free()
+        ntt_dist = {"metric": f"Fr NTT elements/sec @2^{log_n}, one transform block-distributed over {world} GPUs",
+                    "value": n_ntt / fd_s, "unit": "elements/s", "ms_per_ntt": fd_s * 1e3, "scaling": "strong",
+                    "exchange": "3 RCCL all-to-alls of 32*m*(N-1)/N B per rank (dfft.hip)"}
+
+    # ------------------------------------------------------------ oracle leg (rank 0): checks + CPU baseline
     # The CPU oracle (oracle/) is used only here: as the checker and as the
     # timed CPU baseline, never on the measured path.
     checks = {}
     cpu_baseline = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import coracle as co
 
-        # MSM known answer: sum_i s_i (a + i b) mod r, times G (SURVEY §8c KAT), full size
-        kat = co.kat_scalar(cid, a_loc, KAT_B, scal, nthreads=args.cpu_threads)
+        # MSM known answer over all 2^26 terms (SURVEY §8c KAT), every rank's shard
+        shards = [(i0, n_loc, scal, a_loc)] if world == 1 else None
+        kat = msm_kat_scalar(co, cid, world, n_total, r_int, nthreads, shards)
         want = co.jac_to_affine(cid, co.gen_mul(cid, kat))
-        got = co.jac_to_affine(cid, result)
+        got = co.jac_to_affine(cid, msm_result)
         checks[f"msm_kat_2^{args.msm_log}"] = bool(want is not None and got is not None and (want == got).all())
         # NTT: fresh transform of the seeded input vs CPU parallel_fft (fft_cpu.rs:59-111), bit-exact
         d_ntt.write(ntt_in)
         ntt_step()
         gpu_out = d_ntt.read(shape=(n_ntt, 4))
-        lt = min(4, log_n)
+        lt = max(0, min(log_n - 1, nthreads.bit_length() - 1))  # worker.log_num_threads()
         t_cpu = time.perf_counter()
         ref = co.parallel_fft(fr_fid, ntt_in, omega_m, log_n, lt)
         ntt_cpu_s = time.perf_counter() - t_cpu
+        print(f"CPU ({1 << lt} cores) took {ntt_cpu_s * 1e3:.0f}ms", file=sys.stderr)  # tests/fft.rs:77
         checks[f"ntt_vs_parallel_fft_2^{log_n}"] = bool((gpu_out == ref).all())
-        # CPU baseline: multiexp_cpu restatement on a bounded sample of the same workload
-        ns = 1 << args.msm_cpu_log
-        sb = co.gen_bases(cid, 3, 5, ns, nthreads=args.cpu_threads)
-        ss = np.ascontiguousarray(scal[:ns]) if ns <= n_loc else rand_scalars(rng, ns, r_int)
-        t_cpu = time.perf_counter()
-        co.multiexp_cpu(cid, sb, ss, nthreads=args.cpu_threads)
-        cpu_s = time.perf_counter() - t_cpu
-        cpu_baseline = {
-            "value": ns / cpu_s, "unit": "point-adds/s", "cores": args.cpu_threads, "kind": "port",
-            "sample": f"multiexp_cpu restatement (oracle/oracle.c; c=ceil(ln N), windows in parallel) on "
-                      f"2^{args.msm_cpu_log} terms of the same generator: {cpu_s:.2f} s wall",
-            "ntt": {"value": n_ntt / ntt_cpu_s, "unit": "elements/s", "cores": 1 << lt, "kind": "port",
-                    "sample": f"parallel_fft restatement at the full 2^{log_n}: {ntt_cpu_s:.2f} s wall"},
-        }
+        if dist_digests is not None:
+            checks[f"ntt_dist_{world}gpu_vs_parallel_fft_2^{log_n}"] = dist_digests == block_digests(ref, world)
+        if world == 1 and not args.no_cpu_baseline:
+            # CPU baseline: multiexp_cpu restatement on a bounded sample of the same workload
+            ns = min(1 << args.msm_cpu_log, n_loc)
+            sb = np.ascontiguousarray(d_bases.read(shape=(n_loc, 2 * lq))[:ns])
+            ss = np.ascontiguousarray(scal[:ns])
+            t_cpu = time.perf_counter()
+            co.multiexp_cpu(cid, sb, ss, nthreads=nthreads)
+            cpu_s = time.perf_counter() - t_cpu
+            print(f"CPU ({nthreads} cores) took {cpu_s * 1e3:.0f}ms (multiexp_cpu, {ns} terms)", file=sys.stderr)
+            del sb
+            cpu_baseline = {
+                "value": ns / cpu_s, "unit": "point-adds/s", "cores": nthreads, "kind": "port",
+                "sample": f"multiexp_cpu restatement (oracle/oracle.c; c=ceil(ln N), windows in parallel) on the "
+                          f"first 2^{ns.bit_length() - 1} terms of the same inputs: {cpu_s:.2f} s wall",
+                "ntt": {"value": n_ntt / ntt_cpu_s, "unit": "elements/s", "cores": 1 << lt, "kind": "port",
+                        "sample": f"parallel_fft restatement at the full 2^{log_n}: {ntt_cpu_s:.2f} s wall"},
+            }
 
     # ------------------------------------------------------------ end-to-end API (PCIe-inclusive), N = 1
     # The reference API takes host slices and copies them in and out on every
-    # call (multiexp.rs:163-164, fft.rs:89,129).  Not `value`: DESIGN.md §4.
+    # call (multiexp.rs:163-164, fft.rs:89,129).  Not `value`: DESIGN.md §6.
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
         host_bases = d_bases.read(shape=(n_loc, 2 * lq))
@@ -305,7 +357,7 @@ def main():
         t_e = time.perf_counter()
         out_e2e = kern.multiexp(pool, host_bases, scal, 0)
         msm_e2e_s = time.perf_counter() - t_e
-        checks["msm_e2e_equals_resident"] = bool((out_e2e == result).all())
+        checks["msm_e2e_equals_resident"] = bool((out_e2e == msm_result).all())
         fk = ecgpu.FftKernel.create([prog], args.curve + "_fr")
         host_ntt = ntt_in.copy()
         fk.radix_fft(host_ntt, omega_m, log_n)
@@ -341,7 +393,7 @@ def main():
         one = u64(((1 << (64 * lq)) % (P_BLS if cid == 0 else P_BN)), lq)
         jac = np.ascontiguousarray(np.concatenate([aff, np.tile(one, (1 << le, 1))], axis=1))
         d_jac = ecgpu.DeviceBuffer.upload(prog, jac)
-        om_e = omega_for(le)
+        om_e = omega_for(cid, r_int, le)
         ecgpu.ec_fft_dev(prog, args.curve, d_jac, om_e, le)
         d_jac.write(jac)
         t_a = time.perf_counter()
@@ -350,22 +402,32 @@ def main():
         aux["ec_fft"] = {"log_n": le, "ms": ef_s * 1e3, "butterflies_per_s": (1 << (le - 1)) * le / ef_s}
 
     if rank != 0:
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
+        group.barrier()
+        group.close()
         return
 
     # ------------------------------------------------------------ report
+    n_acc = n_loc  # terms per accumulation launch on rank 0 (the largest shard)
+    W = -(-(r_int.bit_length() + 1) // 20) if args.msm_log >= 24 else None  # windows at c = 20
     bytes_per_term = 2 * lq * 8 + 32  # 96 B affine + 32 B scalar (BLS12-381), SURVEY §8(d)
-    acc_achieved = bytes_per_term * n_loc / (acc_avg_ms / 1e3) / 1e9
+    hbm_achieved = bytes_per_term * n_acc / (acc_avg_ms / 1e3) / 1e9
     # the committed PMC passes profile the default (BLS12-381, 2^26 / 2^24) run
-    default_run = cid == 0 and args.msm_log == 26 and log_n == 24
+    default_run = cid == 0 and args.msm_log == 26 and log_n == 24 and world == 1
     acc_traffic, acc_src = pmc_traffic("msm_accumulate", streaming_read=False) if default_run else (None, None)
     ntt_traffic, ntt_src = pmc_traffic("ntt_pass", streaming_read=True) if default_run else (None, None)
     ntt_achieved = 64 * n_ntt / (pass_avg_ms / 1e3) / 1e9
-    # VALU evidence: v_mad_u64_u32 issued by the bucket accumulation (10 Fq muls
-    # per XYZZ mixed add, one per term per window) vs the measured MAD roof.
-    W = -(-(r_int.bit_length() + 1) // 20) if args.msm_log >= 24 else None
+    roofline = {"bound": "valu", "kernel": "msm_accumulate", "avg_ms": acc_avg_ms,
+                "traffic": acc_traffic, "traffic_unit": "GB/launch", "traffic_source": acc_src}
+    if W and cid in RR_LIMBS:
+        mads = madd_mads(RR_LIMBS[cid])
+        achieved = n_acc * W * mads / (acc_avg_ms / 1e3) / 1e12
+        roofline.update({"achieved": achieved, "peak": MAD_PEAK_T, "unit": "T v_mad_u64_u32/s",
+                         "frac": achieved / MAD_PEAK_T,
+                         "note": f"{mads} v_mad_u64_u32 per XYZZ mixed add (8M+2S, {RR_LIMBS[cid]} x 29-bit limbs) "
+                                 f"x {W} windows x terms / launch time; peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz"})
+    roofline["hbm"] = {"achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": hbm_achieved / HBM_PEAK_GBS,
+                       "note": "algorithmic 128 B/term (96 B base + 32 B scalar) x terms per launch / launch time"}
     line = {
         "metric": "BLS12-381 G1 MSM point-adds/sec @2^26 + Fr NTT elements/sec @2^24"
         if cid == 0 else "BN254 G1 MSM point-adds/sec + Fr NTT elements/sec",
@@ -383,39 +445,50 @@ def main():
         "config": {"workload": f"{args.curve} G1 MSM 2^{args.msm_log} terms sharded over {world} GPU(s) "
                                f"+ Fr NTT 2^{log_n} per GPU", "msm_terms": n_total, "ntt_log_n": log_n,
                    "parallelism": f"range-shard x{world} + RCCL all-gather of partials" if world > 1 else "single GPU"},
-        "roofline": {"bound": "hbm", "achieved": acc_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": acc_achieved / HBM_PEAK_GBS, "traffic": acc_traffic, "traffic_unit": "GB/launch",
-                     "traffic_source": acc_src,
-                     "kernel": "msm_accumulate", "avg_ms": acc_avg_ms,
-                     "note": "VALU int-MAD bound; achieved = 128 B/term x terms per launch / launch time"},
+        "roofline": roofline,
         "ntt": {"metric": f"Fr NTT elements/sec @2^{log_n}", "value": world * n_ntt / ntt_s,
                 "unit": "elements/s", "ms_per_ntt": ntt_s * 1e3, "scaling": "weak (one transform per GPU)",
                 "ms_kernels_per_ntt": pass_ms / args.steps, "passes": passes_per_ntt,
-                "roofline": {"bound": "hbm", "achieved": ntt_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "roofline": {"bound": "valu", "achieved": ntt_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": ntt_achieved / HBM_PEAK_GBS, "traffic": ntt_traffic,
                              "traffic_unit": "GB/launch", "traffic_source": ntt_src, "kernel": "ntt_pass",
-                             "avg_ms": pass_avg_ms}},
+                             "avg_ms": pass_avg_ms, "note": "HBM fraction of a VALU-bound pass (64 B/element)"}},
+        "ntt_dist": ntt_dist,
         "checks": checks,
         "cpu_baseline": cpu_baseline,
         "e2e_api": e2e,
         "aux": aux,
+        "runtime": runtime,
     }
-    if W:
-        acc_step_ms = acc_ms / args.steps  # every accumulation launch of one MSM
-        rate = n_loc * W * 10 / (acc_step_ms / 1e3) / 1e9
-        line["valu"] = {"kernel": "msm_accumulate", "achieved": rate, "peak": FQ_MIX_PEAK_G[cid],
-                        "unit": "G Fq-mul/s", "frac": rate / FQ_MIX_PEAK_G[cid],
-                        "note": "10 Fq products (8M+2S) per term per window (c=20) / accumulation time, "
-                                "vs the measured reduced-radix 8M+2S product rate"}
     muls = ntt_fr_muls(log_n)
     fr_rate = muls / (pass_ms / args.steps / 1e3) / 1e9
     line["ntt"]["valu"] = {"kernel": "ntt_pass", "achieved": fr_rate, "peak": FR_MUL_PEAK_G,
                            "unit": "G Fr-mul/s", "frac": fr_rate / FR_MUL_PEAK_G,
                            "note": f"{muls / n_ntt:.2f} Fr products per element per transform / kernel time"}
     print(json.dumps(line))
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    group.barrier()
+    group.close()
+
+
+def pmc_traffic(kernel: str, streaming_read: bool):
+    """HBM bytes per launch (GB) from the committed rocprofv3 PMC passes
+    (tools/gpu.sh prof -> profiles/<round>/pmc_fetch_write.json): FETCH_SIZE +
+    WRITE_SIZE.  gfx950 FETCH_SIZE counts half the bytes of wide coalesced
+    streaming reads (MI355X_MICROARCH.md, HBM/rocprofv3 section), so those are
+    doubled; gathers are reported as counted."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_fetch_write.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    for k, v in d.items():
+        if kernel in k:
+            fetch = v["FETCH_SIZE"]["mean_kb"] * 1024 / 1e9
+            write = v["WRITE_SIZE"]["mean_kb"] * 1024 / 1e9
+            return (2 * fetch if streaming_read else fetch) + write, os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 if __name__ == "__main__":

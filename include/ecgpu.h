@@ -75,6 +75,18 @@ void ecg_ctx_destroy(ecg_ctx *ctx);
 int ecg_ctx_info(ecg_ctx *ctx, size_t *mem_bytes, int *compute_units);
 /* Wait for all work on ctx's device (bench barriers). */
 int ecg_ctx_synchronize(ecg_ctx *ctx);
+/* MSM terms per device pass -- SingleMultiexpKernel::n as calc_chunk_size
+ * derives it from Device::memory (multiexp.rs:71-93,109-127): the engine's
+ * per-term workspace against (1 - MEMORY_PADDING) of the device memory minus
+ * the resident base cache.  Longer MSMs run as several passes, the abort
+ * callback polled before each (multiexp.rs:140-144,348-361).
+ * ecg_ctx_set_msm_chunk pins it (1 .. 2^31-1; 0 restores the derived value). */
+int ecg_msm_chunk_size(ecg_ctx *ctx, int curve_id, size_t *out_terms);
+int ecg_ctx_set_msm_chunk(ecg_ctx *ctx, size_t max_terms);
+/* "hip=<version> (<libamdhip64 path>); rccl=<version> (<librccl path>)": the
+ * HIP runtime and RCCL this process actually bound (launchers check it is the
+ * ROCm install's, not another copy loaded earlier into the process). */
+const char *ecg_runtime_info(void);
 const char *ecg_last_error(void);
 const char *ecg_version(void);
 
@@ -131,8 +143,11 @@ int ecg_msm(ecg_ctx *ctx, int curve_id, const uint64_t *bases_xy, const uint64_t
             uint64_t *out_jac, ecg_abort_cb abort_cb, void *user);
 
 /* MultiexpKernel::parallel_multiexp + multiexp (multiexp.rs:324-400):
- * contiguous ceil(n / nctx) ranges, one host thread per context, partial
- * sums folded on the device of ctxs[0]. */
+ * contiguous ceil(n / nctx) ranges, one host thread per context, each range
+ * in device passes of at most ecg_msm_chunk_size terms, first error wins
+ * (the other workers stop at their next pass), partial sums folded on the
+ * host (multiexp.rs:394-397).  A context listed twice is used by one thread
+ * at a time (every call holds its context's lock). */
 int ecg_msm_multi(ecg_ctx **ctxs, int nctx, int curve_id, const uint64_t *bases_xy,
                   const uint64_t *scalars, size_t n, uint64_t *out_jac, ecg_abort_cb abort_cb,
                   void *user);
@@ -191,7 +206,8 @@ void ecg_base_cache_clear(ecg_ctx *ctx);
 
 /* Sum `count` Jacobian points (3 x Lq u64 each, device memory) into one
  * normalised Jacobian point: the EC fold that follows the RCCL all-gather of
- * per-GPU partials (RCCL has no EC-add reduction op).  out is host memory. */
+ * per-GPU partials (RCCL has no EC-add reduction op).  The points are copied
+ * to the host and folded there (a few adds); out is host memory. */
 int ecg_point_sum_dev(ecg_ctx *ctx, int curve_id, const void *d_points, size_t count,
                       uint64_t *out_jac, void *stream);
 /* Same fold over host memory (multiexp.rs:394-397 cross-device sum). */
@@ -214,8 +230,9 @@ void ecg_comm_destroy(ecg_ctx *ctx);
 int ecg_comm_allgather(ecg_ctx *ctx, const void *d_send, void *d_recv, size_t bytes);
 int ecg_comm_alltoall(ecg_ctx *ctx, const void *d_send, void *d_recv, size_t bytes_per_peer);
 /* MSM over this rank's contiguous shard (multiexp.rs:332-336 split); the
- * partials are all-gathered over RCCL and folded (multiexp.rs:394-397), so
- * every rank gets the full result in out_jac (host, 3 x Lq u64). */
+ * per-rank partial points are all-gathered over RCCL and folded on the host
+ * (multiexp.rs:394-397; RCCL has no EC-add reduction), so every rank gets
+ * the full result in out_jac (host, 3 x Lq u64). */
 int ecg_msm_dist(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n_local,
                  uint64_t *out_jac);
 /* One NTT of 2^log_n points, block-distributed (rank r holds points

@@ -1,9 +1,16 @@
-"""world_size-2 multi-process test (gloo on CPU) of the sharded MSM
-orchestration used by bench.py on N GPUs: contiguous range shards, all-gather
-of the per-rank partial points, fold.  On the GPU the partials come from
-ecg_msm_dev and the fold from ecg_point_sum_dev over RCCL; here both are the
-CPU oracle so the orchestration itself is what is tested."""
+"""world_size-2 multi-process CPU tests of the N>1 path bench.py runs.
+
+* test_bench_dist_path_world2: two processes run bench.py's own host-side
+  orchestration -- ecgpu.dist.HostGroup (the launch's control channel),
+  comm_init's RCCL-id broadcast (with an injected id maker: no RCCL on CPU),
+  bench.msm_shard's contiguous shards and seeds, the all-gather of per-rank
+  partial points and their fold, the max-over-ranks timing reduction, and
+  bench.msm_kat_scalar's full-size known answer regenerated on rank 0.  The
+  per-rank partial comes from the CPU oracle instead of ecg_msm_dist.
+* test_msm_sharded_gloo_world2: the same split through torch.distributed over
+  gloo (ecgpu.dist.msm_sharded / torch_broadcast)."""
 import os
+import socket
 import sys
 
 import numpy as np
@@ -12,7 +19,89 @@ import pytest
 from conftest import ROOT
 
 
-def _worker(rank, world, port, q):
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _fold(co, cid, parts):
+    nq = 6 if cid == 0 else 4
+    acc = np.zeros(3 * nq, dtype=np.uint64)
+    for p in parts:
+        p = np.ascontiguousarray(p, dtype=np.uint64)
+        co.lib().orc_jac_add(cid, co.ptr(acc), co.ptr(acc), co.ptr(p))
+    return acc
+
+
+def _bench_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "0g-ec-gpu_amd"))
+    import bench
+    import coracle as co
+    from ecgpu import dist as edist
+
+    group = edist.HostGroup(rank, world, "127.0.0.1", port)
+    try:
+        ident = edist.comm_init(None, rank, world, group.broadcast, make_id=lambda: bytes(range(128)))
+        ids = group.allgather(ident)
+        ok_id = all(i == bytes(range(128)) for i in ids)
+        for cid, r_int in ((0, bench.R_BLS), (1, bench.R_BN)):
+            n_total = 1001
+            i0, n_loc, scal, a_loc = bench.msm_shard(rank, world, n_total, r_int)
+            assert (i0, i0 + n_loc) == edist.shard_range(n_total, world, rank)
+            B = co.gen_bases(cid, a_loc, bench.KAT_B, n_loc, 2)
+            part = co.multiexp_cpu(cid, B, scal, nthreads=2).reshape(-1)
+            parts = group.allgather(part)
+            got = _fold(co, cid, parts)
+            if rank == 0:
+                kat = bench.msm_kat_scalar(co, cid, world, n_total, r_int, 2)
+                want = co.gen_mul(cid, kat)
+                ok_id = ok_id and bool((co.jac_to_affine(cid, got) == co.jac_to_affine(cid, want)).all())
+        t = group.max(0.5 + rank)
+        group.barrier()
+        q.put((rank, ok_id and t == 0.5 + world - 1))
+    finally:
+        group.close()
+
+
+@pytest.mark.timeout(300)
+def test_bench_dist_path_world2():
+    import multiprocessing as mp
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    results = dict(q.get(timeout=10) for _ in range(2))
+    assert all(p.exitcode == 0 for p in procs)
+    assert results == {0: True, 1: True}
+
+
+def test_kat_scalar_regeneration_matches_single_rank():
+    """bench.msm_kat_scalar over 3 regenerated shards == the KAT of the
+    concatenated scalars: the N>1 check covers exactly the full workload."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import coracle as co
+
+    n, world = 1000, 3
+    shards = [bench.msm_shard(r, world, n, bench.R_BLS) for r in range(world)]
+    allsc = np.ascontiguousarray(np.concatenate([s[2] for s in shards]))
+    assert allsc.shape == (n, 4)
+    k1 = bench.msm_kat_scalar(co, 0, world, n, bench.R_BLS, 2)
+    k2 = co.kat_scalar(0, bench.KAT_A, bench.KAT_B, allsc, nthreads=2)
+    assert k1 == k2
+
+
+def _gloo_worker(rank, world, port, q):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "0g-ec-gpu_amd"))
     import torch
@@ -20,53 +109,42 @@ def _worker(rank, world, port, q):
 
     import coracle as co
     import py_oracle as po
-    from ecgpu.dist import msm_sharded
+    from ecgpu.dist import comm_init, msm_sharded, torch_broadcast
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        ident = comm_init(None, rank, world, torch_broadcast(dist), make_id=lambda: b"\x07" * 128)
         cid, n = 0, 777
         rng = po.Xoshiro256ss(4242)  # same inputs on every rank
         B = co.gen_bases(cid, 31, 37, n, 2)
         E = co.u64arr([rng.field_element(po.BLS12_381_FR) for _ in range(n)], 4)
 
         def partial(i0, i1):
-            p = co.multiexp_cpu(cid, B[i0:i1], E[i0:i1], nthreads=2) if i1 > i0 else \
+            p = co.multiexp_cpu(cid, B[i0:i1], E[i0:i1], nthreads=2).reshape(-1) if i1 > i0 else \
                 co.u64arr([0, 1, 0], 6).reshape(-1)  # identity (0, 1, 0)
-            if i1 > i0:
-                p = p.reshape(-1)
             return torch.from_numpy(p.view(np.int64).copy())
 
         def fold(parts):
-            acc = np.zeros(18, dtype=np.uint64)
-            acc[6:12] = co.u64arr([1], 6)[0]  # placeholder y; z = 0 means identity
-            for t in parts:
-                p = t.numpy().view(np.uint64).copy()
-                co.lib().orc_jac_add(cid, co.ptr(acc), co.ptr(acc), co.ptr(p))
-            return acc
+            return _fold(co, cid, [t.numpy().view(np.uint64) for t in parts])
 
         got = msm_sharded(n, partial, fold)
         want = co.multiexp_cpu(cid, B, E, nthreads=2)
         ok = bool((co.jac_to_affine(cid, got) == co.jac_to_affine(cid, want)).all())
-        q.put((rank, ok))
+        q.put((rank, ok and ident == b"\x07" * 128))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
 def test_msm_sharded_gloo_world2():
-    import socket
-
     import torch.multiprocessing as mp
 
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

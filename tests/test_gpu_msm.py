@@ -116,6 +116,64 @@ def test_msm_ragged_window_padded(kernels, cname, cid):
                           co.multiexp_cpu(cid, B, E, nthreads=16)), n
 
 
+def plan_c(n, nbits):
+    """Window bits make_plan (msm_impl.hpp) picks for n terms: the c >= 2
+    minimising n W + 4 W 2^(c-1) + 12 W c, W = ceil((nbits + 1) / c)."""
+    best = None
+    for c in range(2, 23):
+        w = -(-(nbits + 1) // c)
+        cost = n * w + w * (1 << (c - 1)) * 4 + w * c * 12
+        if best is None or cost < best[0]:
+            best = (cost, c)
+    return best[1]
+
+
+CFG3 = [pytest.param(name, cid, kind, id=f"{name}-{kind}-c{plan_c(1 << 20, 255 if cid == 0 else 254)}")
+        for name, cid in CURVES for kind in ("uniform", "cycled")]
+
+
+@pytest.mark.parametrize("cname,cid,kind", CFG3)
+def test_msm_2p20_config3(kernels, cname, cid, kind):
+    """BASELINE config 3 at its stated size: G1 Pippenger MSM over exactly 2^20
+    terms against multiexp_cpu, with uniform inputs and with the
+    ag-cuda-ec/benches/multiexp.rs:24-26 inputs (bases cycled with period 99,
+    scalars with period 73); the test id names the window bits the plan uses."""
+    cv = po.CURVES[cname]
+    n = 1 << 20
+    if kind == "uniform":
+        B = co.gen_bases(cid, 1000 + cid, 77, n, 16)
+        E = np.ascontiguousarray(rand_scalars_np(cv, n, 2020 + cid))
+    else:
+        B = np.ascontiguousarray(np.tile(co.gen_bases(cid, 41, 43, 99, 4), (n // 99 + 1, 1))[:n])
+        E = np.ascontiguousarray(np.tile(rand_scalars(cv, 73, 73 + cid), (n // 73 + 1, 1))[:n])
+    gpu = kernels[cname].multiexp(ecgpu.Worker(), B, E, 0)
+    assert normalised_form_ok(cid, gpu)
+    assert same_point(cid, gpu, co.multiexp_cpu(cid, B, E, nthreads=16))
+
+
+def rand_scalars_np(cv, n, seed):
+    """uniform scalars < r (numpy rejection sampling; fast at 2^20)."""
+    r = cv.fr.modulus
+    rng = np.random.default_rng(seed)
+    out = np.empty((0, 4), dtype=np.uint64)
+    top = np.uint64((1 << (r.bit_length() - 192)) - 1)
+    while out.shape[0] < n:
+        c = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+        c[:, 3] &= top
+        out = np.concatenate([out, c[_lt_r(c, r)]])
+    return out[:n]
+
+
+def _lt_r(c, r):
+    rl = [np.uint64((r >> (64 * i)) & (2**64 - 1)) for i in range(4)]
+    lt = np.zeros(c.shape[0], dtype=bool)
+    eq = np.ones(c.shape[0], dtype=bool)
+    for k in (3, 2, 1, 0):
+        lt |= eq & (c[:, k] < rl[k])
+        eq &= c[:, k] == rl[k]
+    return lt
+
+
 def test_msm_cycled_bases_and_scalars(kernels):
     """ag-cuda-ec/benches/multiexp.rs:24-26 inputs: bases cycled with period 99,
     scalars with period 73 -- heavy bucket skew and P + P additions."""

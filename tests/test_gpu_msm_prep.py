@@ -102,3 +102,24 @@ def test_multiple_multiexp_montgomery_exps(gpu_programs):
     b = ecgpu.multiple_multiexp(prog, d_b, co.to_mont(0, exps), chunks, exps_montgomery=True)
     for x, y in zip(a, b):
         assert same(0, x, y)
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_base_cache_not_stale(kernels, cname, cid):
+    """A cached entry is keyed by the host address; an array with other
+    content at the same address (a freed array's memory reused) must not be
+    served the old bases: the content fingerprint catches it."""
+    cv = po.CURVES[cname]
+    k = kernels[cname]
+    n = 2048
+    buf = co.gen_bases(cid, 41, 42, n)
+    exps = rand_scalars(cv, n, 77 + cid)
+    got1 = k.multiexp_ex(buf, exps, cache_bases=True)
+    assert same(cid, got1, co.multiexp_cpu(cid, buf, exps, nthreads=8))
+    buf[:] = co.gen_bases(cid, 43, 44, n)   # same address, every record different
+    got2 = k.multiexp_ex(buf, exps, cache_bases=True)
+    assert same(cid, got2, co.multiexp_cpu(cid, buf, exps, nthreads=8))
+    # a temporary copy cannot be cached by address
+    with pytest.raises(ecgpu.EcError, match="cache_bases"):
+        k.multiexp_ex(buf.astype(np.int64), exps, cache_bases=True)
+    k.clear_base_cache()

@@ -10,16 +10,15 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "0g-ec-gpu_amd")]
-import torch.distributed as dist  # noqa: E402
-
 import ecgpu  # noqa: E402
 from ecgpu import dist as edist  # noqa: E402
 
-dist.init_process_group("gloo")
-rank, world = dist.get_rank(), dist.get_world_size()
+group = edist.HostGroup.from_env()
+rank, world = group.rank, group.world
 ndev = ecgpu.lib().ecg_device_count()
 prog = ecgpu.program(ecgpu.Device(int(os.environ.get("LOCAL_RANK", "0")) % ndev))
-edist.comm_init(prog, rank, world, dist)
+print(f"rank {rank}: {ecgpu.lib().ecg_runtime_info().decode()}", flush=True)
+edist.comm_init(prog, rank, world, group.broadcast)
 print(f"rank {rank}/{world}: comm up on device {prog.device.index}", flush=True)
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 log_n = 16
@@ -50,7 +49,7 @@ d_all = ecgpu.DeviceBuffer.upload(prog, e)
 want = ecgpu.msm_dev(prog, "bls12_381", all_b, d_all, nm)
 ok_msm = bool((got == want).all())
 print(f"rank {rank}: fft_dist ok={ok_fft} msm_dist ok={ok_msm}", flush=True)
-dist.barrier()
+group.barrier()
 ecgpu.lib().ecg_comm_destroy(prog.handle)
-dist.destroy_process_group()
+group.close()
 sys.exit(0 if (ok_fft and ok_msm) else 1)
