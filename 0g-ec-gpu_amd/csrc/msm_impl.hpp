@@ -230,8 +230,13 @@ struct KeyMap {
   ECG_DEV uint32_t bucket(uint32_t k) const { return kc ? (k >> kc) * B + (k & (B - 1)) : k; }
 };
 
-// One thread per scalar j of the row; the digits are emitted once per line
-// (entry (w, line, j) at ((w * n_lines + line) * mpad + j)).
+// One thread per scalar j of the row.  Every line of a batched MSM shares
+// the scalar row (ag-cuda-ec/src/multiexp.rs:21-81), so its digits -- and
+// hence the sorted order -- are the same for every line: the entries are
+// emitted and sorted ONCE, entry (w, j) at w * mpad + j with
+// key = (chunk(j) * W + w, |d| - 1) and value = j | sign, and the
+// accumulation walks the sorted list once per line (base and bucket offsets
+// per line).
 template <class C>
 __global__ void __launch_bounds__(MSM_THREADS)
     msm_digits_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, size_t mpad, KeyMap km,
@@ -240,12 +245,11 @@ __global__ void __launch_bounds__(MSM_THREADS)
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= mpad) return;
   if (j >= m) {  // block padding (window-padded mode only): block sentinels
-    for (uint32_t w = 0; w < pl.W; w++)
-      for (uint32_t l = 0; l < g.n_lines; l++) {
-        const size_t o = ((size_t)w * g.n_lines + l) * mpad + j;
-        keys[o] = ((l * pl.W + w) << km.kc) | km.B;
-        vals[o] = 0;
-      }
+    for (uint32_t w = 0; w < pl.W; w++) {
+      const size_t o = (size_t)w * mpad + j;
+      keys[o] = (w << km.kc) | km.B;
+      vals[o] = 0;
+    }
     return;
   }
   uint32_t s[9];
@@ -256,16 +260,14 @@ __global__ void __launch_bounds__(MSM_THREADS)
     const int32_t d = window_digit(s, w, pl, carry);
     const uint32_t mag = d < 0 ? (uint32_t)(-d) : (uint32_t)d;
     const uint32_t sign = d < 0 ? 0x80000000u : 0u;
-    for (uint32_t l = 0; l < g.n_lines; l++) {
-      const size_t o = ((size_t)w * g.n_lines + l) * mpad + j;
-      const uint32_t grp = (l * g.n_chunks + chunk) * pl.W + w;
-      if (d == 0) {
-        keys[o] = km.kc ? (grp << km.kc) | km.B : km.sentinel;
-        vals[o] = 0;
-      } else {
-        keys[o] = km.kc ? (grp << km.kc) | (mag - 1) : grp * pl.B + (mag - 1);
-        vals[o] = (uint32_t)(l * g.line_len + j) | sign;
-      }
+    const size_t o = (size_t)w * mpad + j;
+    const uint32_t grp = chunk * pl.W + w;
+    if (d == 0) {
+      keys[o] = km.kc ? (grp << km.kc) | km.B : km.sentinel;
+      vals[o] = 0;
+    } else {
+      keys[o] = km.kc ? (grp << km.kc) | (mag - 1) : grp * pl.B + (mag - 1);
+      vals[o] = (uint32_t)j | sign;
     }
   }
 }
@@ -329,28 +331,47 @@ ECG_DEV void limb_sel(Fp2<P>& r, bool c, const Fp2<P>& s) {
 #define ECG_ACC_ATTR
 #endif
 
+// Lines (batched MSM): thread ta works on segment t = ta / n_lines of line
+// l = ta % n_lines -- the lanes of a wave walk the same sorted entries for
+// neighbouring lines (same run boundaries, shared key loads) -- with base
+// offset l * line_len and bucket offset l * line_buckets; its records go to
+// slot l * nseg + t, so the record keys stay sorted line-major.
+struct AccLines {
+  uint32_t n_lines;
+  size_t line_len;      // bases per line
+  uint32_t line_buckets;  // buckets per line (n_chunks * W * B)
+};
+
 template <class F>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
     msm_accumulate_kernel(const F* __restrict__ bases, const uint32_t* __restrict__ keys,
-                          const uint32_t* __restrict__ vals, size_t total, KeyMap km, uint32_t seg, size_t t0,
-                          size_t t1, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ recs,
+                          const uint32_t* __restrict__ vals, size_t total, KeyMap km, uint32_t seg, size_t nseg,
+                          AccLines ln, XYZZ<F>* __restrict__ buckets, XYZZ<F>* __restrict__ recs,
                           uint32_t* __restrict__ rkeys) {
-  const size_t t = t0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // segment
-  if (t >= t1) return;
+  const size_t ta = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ta >= nseg * ln.n_lines) return;
+  size_t t = ta;
+  uint32_t l = 0;
+  if (ln.n_lines > 1) {
+    t = ta / ln.n_lines;
+    l = (uint32_t)(ta - t * ln.n_lines);
+  }
+  const size_t slot = (size_t)l * nseg + t;
+  const F* lb = base_ptr(bases, (size_t)l * ln.line_len);
+  const uint32_t boff = l * ln.line_buckets;
   const size_t e0 = t * seg;
-  if (e0 >= total) return;
   const size_t e1 = e0 + seg < total ? e0 + seg : total;
   const XYZZ<F> zero = xyzz_zero<F>();
   uint32_t b = keys[e0];
   if (km.sent(b)) {  // all-zero-digit tail: no records
-    store_xyzz(&recs[2 * t], zero);
-    store_xyzz(&recs[2 * t + 1], zero);
-    rkeys[2 * t] = KEY_END;
-    rkeys[2 * t + 1] = KEY_END;
+    store_xyzz(&recs[2 * slot], zero);
+    store_xyzz(&recs[2 * slot + 1], zero);
+    rkeys[2 * slot] = KEY_END;
+    rkeys[2 * slot + 1] = KEY_END;
     return;
   }
   uint32_t v = vals[e0];
-  Affine<F> P = load_affine(base_ptr(bases, v & 0x7fffffffu));
+  Affine<F> P = load_affine(base_ptr(lb, v & 0x7fffffffu));
   XYZZ<F> acc = zero;
   bool first_run = true;
   for (size_t e = e0; e < e1; e++) {
@@ -359,10 +380,8 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
     const uint32_t kn = more ? keys[e + 1] : KEY_END;
     const uint32_t vn = more ? vals[e + 1] : 0u;
     const bool last = km.sent(kn);  // end of segment or of the block's non-zero digits
-#ifndef ECG_ACC_NOPREFETCH
     Affine<F> Pn;
-    if (!last) Pn = load_affine(base_ptr(bases, vn & 0x7fffffffu));
-#endif
+    if (!last) Pn = load_affine(base_ptr(lb, vn & 0x7fffffffu));
     if (!aff_is_identity(P)) {  // GpuRepr identity (impls.rs:52-54) contributes nothing
       const F ny = pa_neg_y(P.y);  // k p - y: one subtraction (lazy range)
       // per-limb select: a whole-struct `if (neg) P.y = ny` lets the compiler
@@ -371,19 +390,19 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
       acc = pa_add_affine(acc, P);
     }
     if (kn != b) {
-      const uint32_t bi = km.bucket(b);
+      const uint32_t bi = km.bucket(b) + boff;
       if (first_run) {
-        store_xyzz(&recs[2 * t], acc);
-        rkeys[2 * t] = bi;
+        store_xyzz(&recs[2 * slot], acc);
+        rkeys[2 * slot] = bi;
         if (last) {
-          store_xyzz(&recs[2 * t + 1], zero);
-          rkeys[2 * t + 1] = bi;
+          store_xyzz(&recs[2 * slot + 1], zero);
+          rkeys[2 * slot + 1] = bi;
           return;
         }
         first_run = false;
       } else if (last) {
-        store_xyzz(&recs[2 * t + 1], acc);
-        rkeys[2 * t + 1] = bi;
+        store_xyzz(&recs[2 * slot + 1], acc);
+        rkeys[2 * slot + 1] = bi;
         return;
       } else {
         store_xyzz(&buckets[bi], acc);  // interior run: a whole bucket
@@ -391,11 +410,7 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
       acc = zero;
       b = kn;
     }
-#ifndef ECG_ACC_NOPREFETCH
     P = Pn;
-#else
-    if (!last) P = load_affine(base_ptr(bases, vn & 0x7fffffffu));
-#endif
     v = vn;
   }
 }
@@ -715,14 +730,16 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   // window-padded keys (KeyMap) when every (window, line) block is one group
   // and large enough for a sort of its own
   const bool pw = msm_pw_enabled() && g.n_chunks == 1 && m >= ((size_t)1 << 16) &&
-                  ((uint64_t)pl.G << pl.c) < 0xffffffffull;
+                  ((uint64_t)(pl.G / g.n_lines) << pl.c) < 0xffffffffull;
   const size_t mpad = pw ? (m + pl.seg - 1) / pl.seg * pl.seg : m;
-  const size_t nblk = (size_t)pl.W * g.n_lines;
-  const size_t total = nblk * mpad;
-  const KeyMap km{pw ? pl.c : 0u, pl.B, sentinel};
+  // one line's entries (every line shares the scalar row; see msm_digits_kernel)
+  const uint32_t line_groups = pl.G / g.n_lines;  // n_chunks * W
+  const size_t total = (size_t)pl.W * mpad;
+  const KeyMap km{pw ? pl.c : 0u, pl.B, line_groups * pl.B};
   int key_bits = 1;
-  while ((1ull << key_bits) <= sentinel) key_bits++;
-  const size_t nseg = (total + pl.seg - 1) / pl.seg;
+  while ((1ull << key_bits) <= km.sentinel) key_bits++;
+  const size_t nseg = (total + pl.seg - 1) / pl.seg;        // segments of the sorted list
+  const size_t nseg_all = nseg * g.n_lines;                 // accumulation threads (all lines)
 
   void *k0, *k1, *v0, *v1, *bk, *rc, *rk, *rc2, *rk2, *pa, *pb, *tmp;
   ECG_TRY(ws_get(ctx, "msm_k0", total * 4, &k0));
@@ -730,9 +747,9 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   ECG_TRY(ws_get(ctx, "msm_v0", total * 4, &v0));
   ECG_TRY(ws_get(ctx, "msm_v1", total * 4, &v1));
   ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nb * sizeof(X), &bk));
-  ECG_TRY(ws_get(ctx, "msm_recs", 2 * nseg * sizeof(X), &rc));
-  ECG_TRY(ws_get(ctx, "msm_rkeys", 2 * nseg * 4, &rk));
-  const size_t nseg1 = (2 * nseg + MSM_COMBINE_SEG - 1) / MSM_COMBINE_SEG;
+  ECG_TRY(ws_get(ctx, "msm_recs", 2 * nseg_all * sizeof(X), &rc));
+  ECG_TRY(ws_get(ctx, "msm_rkeys", 2 * nseg_all * 4, &rk));
+  const size_t nseg1 = (2 * nseg_all + MSM_COMBINE_SEG - 1) / MSM_COMBINE_SEG;
   ECG_TRY(ws_get(ctx, "msm_recs2", 2 * nseg1 * sizeof(X), &rc2));
   ECG_TRY(ws_get(ctx, "msm_rkeys2", 2 * nseg1 * 4, &rk2));
   ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
@@ -777,14 +794,15 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   // (13 launch tails, and the concurrent sort slows the VALU-bound
   // accumulation by as much as it hides)
   ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
-  hipLaunchKernelGGL(msm_accumulate_kernel<F>, dim3(blocks_for(nseg, MSM_THREADS)), dim3(MSM_THREADS), 0, s, bases,
-                     (const uint32_t*)k1, (const uint32_t*)v1, total, km, pl.seg, (size_t)0, nseg, (X*)bk, (X*)rc,
+  const AccLines ln{g.n_lines, g.line_len, line_groups * pl.B};
+  hipLaunchKernelGGL(msm_accumulate_kernel<F>, dim3(blocks_for(nseg_all, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                     bases, (const uint32_t*)k1, (const uint32_t*)v1, total, km, pl.seg, nseg, ln, (X*)bk, (X*)rc,
                      (uint32_t*)rk);
   ECG_HIP(hipGetLastError());
   ECG_TRY(kt_end(ctx, "msm_accumulate", s));
 
   // combine the segment-edge partials, level by level
-  size_t nrec = 2 * nseg;
+  size_t nrec = 2 * nseg_all;
   X* rin = (X*)rc;
   uint32_t* kin = (uint32_t*)rk;
   X* rout = (X*)rc2;

@@ -107,7 +107,7 @@ def parse(argv=None):
     ap.add_argument("--no-check", action="store_true", help="skip the oracle checks (profiling runs)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU baseline threads (default: EC_GPU_NUM_THREADS, else OMP_NUM_THREADS, else affinity)")
-    ap.add_argument("--msm-cpu-log", type=int, default=23)
+    ap.add_argument("--msm-cpu-log", type=int, default=24)
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive API timings (N=1)")
     ap.add_argument("--no-aux", action="store_true", help="skip the batched-MSM / EC-FFT side lines (N=1)")
     return ap.parse_args(argv)
