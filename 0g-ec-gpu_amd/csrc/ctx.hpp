@@ -56,6 +56,7 @@ struct KernelTimes {
 struct ecg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // H2D staging of the host-slice MSM (lazily created)
   std::recursive_mutex mu;  // held by every API call on this context (ECG_ENTER)
   size_t mem_bytes = 0;
   int compute_units = 0;
@@ -145,6 +146,9 @@ int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_base
                   hipStream_t s);
 int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac);
 int msm_pass_terms_run(const ecg_ctx* ctx, int curve_id, size_t* out);
+// MSM over host slices, uploads pipelined with compute (msm_host_t)
+int msm_host_run(ecg_ctx* ctx, int curve_id, const void* h_bases, const void* h_scalars, size_t n, uint64_t* out_jac,
+                 ecg_abort_cb abort_cb, void* user);
 int gen_bases_run(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n,
                   void* d_out, hipStream_t s);
 

@@ -209,6 +209,7 @@ void ecg_ctx_destroy(ecg_ctx* ctx) {
   for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
   base_cache_free(ctx);
   comm_free(ctx);
+  if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -383,19 +384,9 @@ static int msm_host(ecg_ctx* ctx, int curve_id, const uint64_t* bases_xy, const 
     set_error("multiexp: unknown curve_id %d", curve_id);
     return ECG_ERR_INVALID;
   }
-  const size_t lq = fq_limbs64(curve_id);
-  const size_t bb = n * 2 * lq * 8, sb = n * 32;
-  void *db, *ds;
-  ECG_TRY(ws_get(ctx, "msm_in_bases", bb, &db));
-  ECG_TRY(ws_get(ctx, "msm_in_scalars", sb, &ds));
-  hipStream_t s = ctx->stream;
-  if (n) {
-    ECG_HIP(hipMemcpyAsync(db, bases_xy, bb, hipMemcpyHostToDevice, s));  // multiexp.rs:163-164
-    ECG_HIP(hipMemcpyAsync(ds, scalars, sb, hipMemcpyHostToDevice, s));
-  }
-  int rc = msm_run(ctx, curve_id, db, ds, n, out_jac, s, abort_cb, user);
-  (void)hipStreamSynchronize(s);
-  if (rc != ECG_OK) return rc;
+  // multiexp.rs:163-164 copies the slices in; here the copies are pipelined
+  // with the compute pass by pass (msm_host_t)
+  ECG_TRY(msm_host_run(ctx, curve_id, bases_xy, scalars, n, out_jac, abort_cb, user));
   return kt_collect(ctx);
 }
 

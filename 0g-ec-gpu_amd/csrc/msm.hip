@@ -82,6 +82,17 @@ int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count
   return point_sum_host(curve_id, pts.data(), count, out_jac);
 }
 
+int msm_host_run(ecg_ctx* ctx, int curve_id, const void* h_bases, const void* h_scalars, size_t n, uint64_t* out_jac,
+                 ecg_abort_cb abort_cb, void* user) {
+  if (n > 0x7fffffffull) {
+    set_error("multiexp: at most 2^31-1 terms per call");
+    return ECG_ERR_INVALID;
+  }
+  const MsmOps* o = msm_ops(curve_id, "multiexp");
+  if (!o) return ECG_ERR_INVALID;
+  return o->host(ctx, h_bases, h_scalars, n, out_jac, abort_cb, user);
+}
+
 int msm_pass_terms_run(const ecg_ctx* ctx, int curve_id, size_t* out) {
   const MsmOps* o = msm_ops(curve_id, "multiexp");
   if (!o) return ECG_ERR_INVALID;

@@ -867,6 +867,29 @@ int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const M
   return msm_core_impl<C, typename C::Fq>(ctx, d_bases, d_scalars, g, pl, s, d_sums);
 }
 
+// Horner fold of one pass's W window sums (lazy device XYZZ) into `total`
+// on the host (multiexp.rs:221-233).
+template <class C>
+void msm_host_fold(const XYZZ<typename C::Fq>* win, const MsmPlan& pl, host::HPoint<HostF<C>>& total) {
+  using HX = host::HPoint<HostF<C>>;
+  HX acc = HX::zero();
+  for (int w = (int)pl.W - 1; w >= 0; w--) {
+    for (uint32_t k = 0; k < pl.c; k++) acc = host::hdbl(acc);
+    HX ww;
+    static_assert(sizeof(ww.X) == sizeof(win[w].X), "host/device coordinate layouts differ");
+    memcpy(&ww.X, &win[w].X, sizeof(ww.X));
+    memcpy(&ww.Y, &win[w].Y, sizeof(ww.Y));
+    memcpy(&ww.ZZ, &win[w].ZZ, sizeof(ww.ZZ));
+    memcpy(&ww.ZZZ, &win[w].ZZZ, sizeof(ww.ZZZ));
+    ww.X = host::hcanon(ww.X);  // device values are in the lazy range [0, 2p]
+    ww.Y = host::hcanon(ww.Y);
+    ww.ZZ = host::hcanon(ww.ZZ);
+    ww.ZZZ = host::hcanon(ww.ZZZ);
+    acc = host::hadd_pts(acc, ww);
+  }
+  total = host::hadd_pts(total, acc);
+}
+
 // Terms per device pass: calc_chunk_size (multiexp.rs:71-93) restated for
 // this pipeline's workspace.  Per term: the staged input base
 // and scalar (host-slice entry points), the reduced-radix base record, W
@@ -918,28 +941,118 @@ int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_
     win.resize(pl.W);
     ECG_HIP(hipMemcpyAsync(win.data(), d_sums, pl.W * sizeof(X), hipMemcpyDeviceToHost, s));
     ECG_HIP(hipStreamSynchronize(s));
-    HX acc = HX::zero();
-    for (int w = (int)pl.W - 1; w >= 0; w--) {
-      for (uint32_t k = 0; k < pl.c; k++) acc = host::hdbl(acc);
-      HX ww;
-      // device values are in the lazy range [0, 2p]: canonicalise
-      static_assert(sizeof(ww.X) == sizeof(win[w].X), "host/device coordinate layouts differ");
-      memcpy(&ww.X, &win[w].X, sizeof(ww.X));
-      memcpy(&ww.Y, &win[w].Y, sizeof(ww.Y));
-      memcpy(&ww.ZZ, &win[w].ZZ, sizeof(ww.ZZ));
-      memcpy(&ww.ZZZ, &win[w].ZZZ, sizeof(ww.ZZZ));
-      ww.X = host::hcanon(ww.X);
-      ww.Y = host::hcanon(ww.Y);
-      ww.ZZ = host::hcanon(ww.ZZ);
-      ww.ZZZ = host::hcanon(ww.ZZZ);
-      acc = host::hadd_pts(acc, ww);
-    }
-    total_acc = host::hadd_pts(total_acc, acc);
+    msm_host_fold<C>(win.data(), pl, total_acc);
   }
   host::hto_jac_norm(total_acc, out_jac);
   return ECG_OK;
 }
 
+
+static uint32_t msm_h2d_passes() {  // host-slice pipeline depth (A/B: ECG_MSM_H2D_PASSES)
+  static const uint32_t v = env_u32("ECG_MSM_H2D_PASSES", 4);
+  return v ? v : 1;
+}
+
+// MSM over HOST slices -- the reference's own entry (SingleMultiexpKernel::
+// multiexp copies bases and exps in on every call, multiexp.rs:152-164).
+// Instead of copying all 128 B/term and then computing, the terms run as
+// passes whose upload overlaps the previous pass's compute: pass k+1's bases
+// and scalars go H2D on a copy stream into the other half of a double-
+// buffered staging area while the compute stream runs pass k (the
+// accumulation is VALU-bound, the copy is PCIe-bound).  Each pass leaves its
+// W window sums in a device array; one D2H and the host Horner folds follow
+// the last pass.  Same group element as the single-pass MSM.
+template <class C>
+int msm_host_t(ecg_ctx* ctx, const void* h_bases, const void* h_scalars, size_t n, uint64_t* out_jac,
+               ecg_abort_cb abort_cb, void* user) {
+  using F = typename C::Fq;
+  using X = XYZZ<F>;
+  using HX = host::HPoint<HostF<C>>;
+  kt_reset(ctx, "msm_accumulate");
+  if (n == 0) {
+    host::hto_jac_norm(HX::zero(), out_jac);
+    return ECG_OK;
+  }
+  const size_t bb = 2 * sizeof(F), sb = 32;
+  size_t pass = msm_pass_terms<C>(ctx);
+  if (n >= ((size_t)1 << 22)) {
+    const size_t want = (n + msm_h2d_passes() - 1) / msm_h2d_passes();
+    if (want < pass) pass = want;
+  }
+  const size_t np = (n + pass - 1) / pass;
+  std::vector<MsmPlan> plans(np);
+  std::vector<size_t> woff(np + 1, 0);
+  for (size_t k = 0; k < np; k++) {
+    const size_t m = std::min(pass, n - k * pass);
+    plans[k] = make_plan(m, (uint32_t)C::FrParams::BITS);
+    woff[k + 1] = woff[k] + plans[k].W;
+  }
+  void *ib[2] = {nullptr, nullptr}, *is[2] = {nullptr, nullptr}, *sums;
+  ECG_TRY(ws_get(ctx, "msm_in_bases", pass * bb, &ib[0]));
+  ECG_TRY(ws_get(ctx, "msm_in_scalars", pass * sb, &is[0]));
+  if (np > 1) {
+    ECG_TRY(ws_get(ctx, "msm_in_bases_b", pass * bb, &ib[1]));
+    ECG_TRY(ws_get(ctx, "msm_in_scalars_b", pass * sb, &is[1]));
+  }
+  ECG_TRY(ws_get(ctx, "msm_pass_sums", woff[np] * sizeof(X), &sums));
+  if (!ctx->copy_stream) ECG_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  hipStream_t cs = ctx->stream, us = ctx->copy_stream;
+  hipEvent_t up[2], done[2];
+  for (int i = 0; i < 2; i++) {
+    ECG_HIP(hipEventCreateWithFlags(&up[i], hipEventDisableTiming));
+    ECG_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+  }
+  auto upload = [&](size_t k) -> int {
+    const size_t off = k * pass, m = std::min(pass, n - off);
+    const int b = (int)(k & 1);
+    ECG_HIP(hipMemcpyAsync(ib[b], (const uint8_t*)h_bases + off * bb, m * bb, hipMemcpyHostToDevice, us));
+    ECG_HIP(hipMemcpyAsync(is[b], (const uint8_t*)h_scalars + off * sb, m * sb, hipMemcpyHostToDevice, us));
+    ECG_HIP(hipEventRecord(up[b], us));
+    return ECG_OK;
+  };
+  int rc = upload(0);
+  for (size_t k = 0; rc == ECG_OK && k < np; k++) {
+    if (abort_cb && abort_cb(user)) {  // multiexp.rs:140-144, before every pass
+      rc = ECG_ABORTED;
+      break;
+    }
+    const int b = (int)(k & 1);
+    const size_t m = std::min(pass, n - k * pass);
+    const MsmGeom g{1, 1, m, m, 0};
+    void* d_sums = nullptr;
+    rc = [&]() -> int {
+      ECG_HIP(hipStreamWaitEvent(cs, up[b], 0));
+      ECG_TRY(msm_core_t<C>(ctx, ib[b], is[b], g, plans[k], cs, &d_sums));
+      ECG_HIP(hipMemcpyAsync((X*)sums + woff[k], d_sums, plans[k].W * sizeof(X), hipMemcpyDeviceToDevice, cs));
+      ECG_HIP(hipEventRecord(done[b], cs));
+      if (k + 1 < np) {
+        if (k >= 1) ECG_HIP(hipStreamWaitEvent(us, done[b ^ 1], 0));  // pass k-1 has released its staging half
+        ECG_TRY(upload(k + 1));
+      }
+      return ECG_OK;
+    }();
+  }
+  (void)hipStreamSynchronize(us);
+  std::vector<X> win(woff[np]);
+  if (rc == ECG_OK) {
+    rc = [&]() -> int {
+      ECG_HIP(hipMemcpyAsync(win.data(), sums, woff[np] * sizeof(X), hipMemcpyDeviceToHost, cs));
+      ECG_HIP(hipStreamSynchronize(cs));
+      return ECG_OK;
+    }();
+  } else {
+    (void)hipStreamSynchronize(cs);
+  }
+  for (int i = 0; i < 2; i++) {
+    (void)hipEventDestroy(up[i]);
+    (void)hipEventDestroy(done[i]);
+  }
+  if (rc != ECG_OK) return rc;
+  HX total = HX::zero();
+  for (size_t k = 0; k < np; k++) msm_host_fold<C>(win.data() + woff[k], plans[k], total);
+  host::hto_jac_norm(total, out_jac);
+  return ECG_OK;
+}
 
 // Batched multi-line MSM (ag-cuda-ec multiple_multiexp): all tasks in one
 // pass -- one sort over (task, window, bucket) keys, one accumulation launch,

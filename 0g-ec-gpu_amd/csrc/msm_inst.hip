@@ -32,6 +32,7 @@ static int batch_entry(ecg_ctx* ctx, const void* d_bases, const void* d_scalars,
 
 extern MsmOps ECG_OPS_NAME;
 MsmOps ECG_OPS_NAME = {&msm_single_t<InstCurve>, &batch_entry, &point_sum_host_t<InstCurve>,
-                             &gen_bases_t<InstCurve>, &msm_pass_terms<InstCurve>};
+                             &gen_bases_t<InstCurve>, &msm_pass_terms<InstCurve>,
+                             &msm_host_t<InstCurve>};
 
 }  // namespace ecg

@@ -12,6 +12,8 @@ struct MsmOps {
   int (*point_sum)(const uint64_t* points, size_t count, uint64_t* out_jac);
   int (*gen_bases)(ecg_ctx*, const uint64_t* a, const uint64_t* b, size_t n, void* d_out, hipStream_t);
   size_t (*pass_terms)(const ecg_ctx*);
+  int (*host)(ecg_ctx*, const void* h_bases, const void* h_scalars, size_t n, uint64_t* out_jac, ecg_abort_cb,
+              void* user);
 };
 
 }  // namespace ecg
