@@ -564,6 +564,91 @@ ECG_DEV Fp<typename Q::Base> rr_to_std(const FpR<Q>& a) {
 }
 
 // ---------------------------------------------------------------------------
+// carry-free sums / differences and cheap value reduction (the NTT's
+// butterflies, ntt.hip; bounds in the NTT section of DESIGN.md)
+// ---------------------------------------------------------------------------
+// a + b, limb by limb (no carry step)
+template <class Q>
+ECG_DEV FpR<Q> rr_add_nc(const FpR<Q>& a, const FpR<Q>& b) {
+  FpR<Q> r;
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) r.v[i] = a.v[i] + b.v[i];
+  return r;
+}
+
+// a + K p - b, limb by limb (no carry step): limb-wise non-negative when every
+// limb of b is <= 2^(BITS+1) - 2 and value(b) <= K p / 2
+template <int K, class Q>
+ECG_DEV FpR<Q> rr_sub_nc(const FpR<Q>& a, const FpR<Q>& b) {
+  constexpr int j = kp_index<K>();
+  static_assert((Q::KP_OK >> j) & 1, "K p not representable for this field (tools/gen_params_rr.py)");
+  FpR<Q> r;
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) r.v[i] = a.v[i] + Q::KP[j][i] - b.v[i];
+  return r;
+}
+
+// Exact limbs (< 2^BITS below the top limb), same value: sequential carry.
+template <class Q>
+ECG_DEV FpR<Q> rr_carry_seq(const FpR<Q>& a) {
+  constexpr int B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  FpR<Q> r;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < Q::NL - 1; i++) {
+    const uint64_t t = (uint64_t)a.v[i] + c;
+    r.v[i] = (uint32_t)t & MASK;
+    c = (uint32_t)(t >> B);
+  }
+  r.v[Q::NL - 1] = a.v[Q::NL - 1] + c;
+  return r;
+}
+
+// v - q p with q = floor(v_top * floor(2^32 / (P_top + 1)) / 2^32), never
+// above floor(v / p): for limbs < 2^31.4 and value < 64 p the result has
+// exact limbs and value < p (1 + v_top / 2^32) + 2^(BITS (NL-1) + 6) < 1.1 p
+// -- a product-free "mod p, almost".
+template <class Q>
+ECG_DEV FpR<Q> rr_reduce_q(const FpR<Q>& a) {
+  constexpr int NL = Q::NL, B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  constexpr uint32_t MAGIC = (uint32_t)((1ull << 32) / ((uint64_t)Q::P[NL - 1] + 1));
+  const uint32_t q = __umulhi(a.v[NL - 1], MAGIC);
+  FpR<Q> r;
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL - 1; i++) {
+    const int64_t t = (int64_t)a.v[i] + c - (int64_t)((uint64_t)q * Q::P[i]);
+    r.v[i] = (uint32_t)t & MASK;
+    c = t >> B;  // arithmetic
+  }
+  r.v[NL - 1] = (uint32_t)((int64_t)a.v[NL - 1] + c - (int64_t)((uint64_t)q * Q::P[NL - 1]));
+  return r;
+}
+
+// Canonical value (< p) of an exact-limb value < 2p: one conditional
+// subtraction with a sequential borrow.
+template <class Q>
+ECG_DEV FpR<Q> rr_canon_lt2p(const FpR<Q>& a) {
+  constexpr int NL = Q::NL, B = Q::BITS;
+  constexpr uint32_t MASK = (1u << B) - 1;
+  uint32_t t[NL];
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    const int32_t d = (int32_t)a.v[i] - (int32_t)Q::P[i] + br;
+    t[i] = i + 1 < NL ? (uint32_t)d & MASK : (uint32_t)d;
+    br = d >> B;  // 0 or -1 (top limb: sign of the difference)
+  }
+  const bool ge = br == 0;
+  FpR<Q> r;
+#pragma unroll
+  for (int i = 0; i < NL; i++) r.v[i] = ge ? t[i] : a.v[i];
+  return r;
+}
+
+// ---------------------------------------------------------------------------
 // memory: NL words, moved as 16-B vectors where NL allows
 // ---------------------------------------------------------------------------
 template <class Q>

@@ -6,14 +6,16 @@
 // batch of independent 2^deg-point DFTs between a strided gather and a
 // scatter), re-designed for gfx950:
 //
-//  * v2 (default): radix up to 2^12 per pass, so 2^24 is TWO passes (the
-//    reference uses radix-2^8, three passes, fft.rs:15) -- one fewer twiddled
-//    pass and no odd-pass copy back.  A 2^12-point group lives in 128 KiB of
-//    LDS (two 16-byte planes) worked by a 1024-thread workgroup; smaller
-//    radices put G = 1024/2^deg groups in a workgroup so every global read is
-//    a G*32-byte run.  Each thread runs TWO DIF rounds per LDS round trip on 4
-//    register-resident elements (radix-2^2 step), halving LDS traffic and
-//    barriers.
+//  * v2 (default): ceil(log n / 10) balanced passes of radix up to 2^10
+//    (2^24 is three passes of 2^8; ECG_NTT_MAXDEG up to 12 for A/B).  A
+//    pass's groups are packed into 1024-element tiles in LDS worked by
+//    256-thread workgroups, so every global read is a G*32-byte run.  Each
+//    thread runs TWO DIF rounds per LDS round trip on 4 register-resident
+//    elements (radix-2^2 step), halving LDS traffic and barriers.
+//  * The butterflies run in the reduced-radix form (ntt_pass_rr_kernel, see
+//    its header) whenever the full per-pass twiddle tables fit (log n <= 28):
+//    ~1/3 fewer VALU instructions per product.  ECG_NTT_RR=0 keeps the
+//    32-bit-limb passes below for A/B.
 //  * No per-thread exponentiation (the reference's FIELD_pow_lookup + FIELD_pow
 //    per thread, fft.cl:39-45, ~4x the butterfly work): inter-pass twiddles
 //    w^e (e < n) = T_hi[e >> 12] * T_lo[e & 4095] from L2-resident tables;
@@ -27,6 +29,7 @@
 
 #include "ctx.hpp"
 #include "field.hpp"
+#include "fieldrr.hpp"
 
 namespace ecg {
 
@@ -227,6 +230,217 @@ __global__ void __launch_bounds__(256)
   pass_store<F, DEG>(y, U, lgp, log_g, E);
 }
 
+// ---------------------------------------------------------------------------
+// Reduced-radix pass (default for both scalar fields): the same Stockham
+// schedule, with the butterflies in the 9 x 29-bit form of fieldrr.hpp.  An
+// Fr product is then 162 v_mad_u64_u32 and no carry instructions (the 32-bit
+// form above issues 128 mads + 128 addc + the final subtraction), and sums /
+// differences are limb-wise with no carry chain.
+//
+// No conversion product anywhere: the caller's word x R (< r) is re-read as a
+// 9-limb integer, i.e. as the reduced-radix form of x R / R' (R' = 2^261).
+// The transform is linear, so the output integers are y R / R' * R' = y R --
+// exactly the boundary form -- once packed back into 8 words.  Twiddles are
+// stored in the R' form (converted once when the tables are built).
+//
+// Values between butterfly rounds ("E-form"): exact limbs, value <= 2.5 r.
+// A radix-2^2 step on e0..e3 (r / R' <= 2^-6.1; products take one operand
+// with limbs < 2^31.6 against an exact twiddle and return < r (1 + K 2^-6.1)):
+//   s0 = e0 + e2, d0 = (e0 + 8r - e2) w0        (<= 5 r,  <= 1.15 r)
+//   s1 = e1 + e3, d1 = (e1 + 8r - e3) w1
+//   a0 = reduce_q(s0 + s1)                      (<= 1.1 r)
+//   a1 = (s0 + 16r - s1) w2                     (<= 1.3 r)
+//   b0 = carry(d0 + d1)                         (<= 2.3 r)
+//   b1 = (d0 + 4r - d1) w2                      (<= 1.1 r)
+// The last step of a pass (h = 1: three of its four twiddles are 1) uses
+// reduce_q instead of those three products.  In HBM -- pass inputs, outputs
+// and the twiddle tables -- every value is canonical (< r) and packed into
+// the 8-word boundary layout, so the strided Stockham gathers read whole
+// 128-B lines as the 32-bit-limb passes do; the 9-limb form lives only in
+// VGPRs and LDS.
+// ---------------------------------------------------------------------------
+template <class Q>
+struct RrPlanes {  // limbs 0-3 | 4-7 | 8 of element i (NL = 9)
+  uint4* a;
+  uint4* b;
+  uint32_t* c;
+  ECG_HD static RrPlanes over(void* base, size_t n) {
+    uint4* p = reinterpret_cast<uint4*>(base);
+    return RrPlanes{p, p + n, reinterpret_cast<uint32_t*>(p + 2 * n)};
+  }
+  ECG_HD RrPlanes at(size_t off) const { return RrPlanes{a + off, b + off, c + off}; }
+  ECG_DEV FpR<Q> get(size_t i) const {
+    static_assert(Q::NL == 9, "three planes hold 9 limbs");
+    const uint4 x = a[i], y = b[i];
+    FpR<Q> r;
+    r.v[0] = x.x; r.v[1] = x.y; r.v[2] = x.z; r.v[3] = x.w;
+    r.v[4] = y.x; r.v[5] = y.y; r.v[6] = y.z; r.v[7] = y.w;
+    r.v[8] = c[i];
+    return r;
+  }
+  ECG_DEV void put(size_t i, const FpR<Q>& v) const {
+    a[i] = make_uint4(v.v[0], v.v[1], v.v[2], v.v[3]);
+    b[i] = make_uint4(v.v[4], v.v[5], v.v[6], v.v[7]);
+    c[i] = v.v[8];
+  }
+};
+
+template <class Q>
+ECG_DEV FpR<Q> rr_load_std(const uint4* __restrict__ x, size_t i) {  // 8 words x R -> 9 exact limbs
+  const uint4 lo = x[2 * i], hi = x[2 * i + 1];
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  FpR<Q> r;
+  rr_unpack<Q, 8>(w, r.v);
+  return r;
+}
+
+template <class Q>
+ECG_DEV void rr_store_std(uint4* __restrict__ y, size_t i, const FpR<Q>& v) {  // E-form -> canonical 8 words
+  const FpR<Q> c = rr_canon_lt2p(rr_reduce_q(v));
+  uint32_t w[8];
+  rr_pack<Q, 8>(c.v, w);
+  y[2 * i] = make_uint4(w[0], w[1], w[2], w[3]);
+  y[2 * i + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
+// 256-thread workgroups (tiles of <= 1024 elements): at the 1024-thread bound
+// (128 VGPRs) the products spilled
+constexpr uint32_t NTT_RR_THREADS = 512;
+
+#ifndef ECG_NTT_RR_WAVES
+#define ECG_NTT_RR_WAVES 4
+#endif
+template <class Q, int DEG>
+__global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_per_eu(ECG_NTT_RR_WAVES)))
+    ntt_pass_rr_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, const uint4* __restrict__ pq,
+                       uint32_t pq_shift, const uint4* __restrict__ twf, uint32_t log_n, uint32_t lgp,
+                       uint32_t log_g) {
+  using F = FpR<Q>;
+  constexpr uint32_t R = 1u << DEG;
+  extern __shared__ uint4 smem[];
+  const uint32_t E = R << log_g;
+  const RrPlanes<Q> U = RrPlanes<Q>::over(smem, E);
+  const uint32_t G = 1u << log_g;
+  const size_t n = (size_t)1 << log_n;
+  const uint64_t g0 = (uint64_t)blockIdx.x << log_g;
+
+  // ---- load: u[i] = x[g + i t] * w^((n >> (lgp + DEG)) k i) (full per-pass table)
+  {
+    const uint64_t t = n >> DEG;
+    const uint64_t p = 1ull << lgp;
+    F v[NTT_EPT];
+#pragma unroll
+    for (int q = 0; q < NTT_EPT; q++) {
+      const uint32_t f = threadIdx.x + q * blockDim.x;
+      v[q] = F::zero();
+      if (f < E) {
+        const uint64_t src = g0 + (f & (G - 1)) + (uint64_t)(f >> log_g) * t;
+        v[q] = rr_load_std<Q>(x, src);
+      }
+    }
+    if (lgp != 0) {  // every element times its twiddle (w^0 = 1 is a table entry too: no divergence)
+      F w[NTT_EPT];
+#pragma unroll
+      for (int q = 0; q < NTT_EPT; q++) {
+        const uint32_t f = threadIdx.x + q * blockDim.x;
+        const uint64_t g = g0 + (f & (G - 1));
+        w[q] = f < E ? rr_load_std<Q>(twf, (uint64_t)(f >> log_g) * p + (g & (p - 1))) : F::one();
+      }
+#pragma unroll
+      for (int q = 0; q + 1 < NTT_EPT; q += 2) {
+        F p0, p1;
+        rr_mul2(v[q], w[q], v[q + 1], w[q + 1], p0, p1);
+        v[q] = p0;
+        v[q + 1] = p1;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NTT_EPT; q++) {
+      const uint32_t f = threadIdx.x + q * blockDim.x;
+      if (f < E) U.put(((f & (G - 1)) << DEG) + (f >> log_g), v[q]);
+    }
+  }
+  __syncthreads();
+
+  // ---- radix-2^2 steps (rounds r, r+1 of the DIF network)
+  int r = 0;
+  constexpr uint32_t RQ = R >= 4 ? R / 4 : 1;
+#pragma unroll 1
+  for (; r + 1 < DEG; r += 2) {
+    const uint32_t bit = (R / 2) >> r, h = bit >> 1;
+    for (uint32_t f = threadIdx.x; f < E / 4; f += blockDim.x) {
+      const uint32_t gi = f / RQ, q = f % RQ;
+      const uint32_t qm = q & (h - 1);
+      const uint32_t j = (gi << DEG) + ((q / h) * (2 * bit)) + qm;
+      const F e0 = U.get(j), e1 = U.get(j + h), e2 = U.get(j + bit), e3 = U.get(j + bit + h);
+      const F s0 = rr_add_nc(e0, e2), s1 = rr_add_nc(e1, e3);
+      F a0, a1, b0, b1;
+      if (h > 1) {
+        F d0, d1, a1p, b1p;
+        rr_mul2(rr_sub_nc<8>(e0, e2), rr_load_std<Q>(pq, (size_t)(qm << r) << pq_shift), rr_sub_nc<8>(e1, e3),
+                rr_load_std<Q>(pq, (size_t)((qm + h) << r) << pq_shift), d0, d1);
+        a0 = rr_reduce_q(rr_add_nc(s0, s1));
+        b0 = rr_carry_seq(rr_add_nc(d0, d1));
+        const F w2 = rr_load_std<Q>(pq, (size_t)(qm << (r + 1)) << pq_shift);
+        rr_mul2(rr_sub_nc<16>(s0, s1), w2, rr_sub_nc<4>(d0, d1), w2, a1p, b1p);
+        a1 = a1p;
+        b1 = b1p;
+      } else {  // h = 1: qm = 0, so d1's twiddle w^(1 << r) is the only non-trivial one
+        const F d0 = rr_reduce_q(rr_sub_nc<8>(e0, e2));
+        const F d1 = rr_mul(rr_sub_nc<8>(e1, e3), rr_load_std<Q>(pq, (size_t)(1u << r) << pq_shift));
+        a0 = rr_reduce_q(rr_add_nc(s0, s1));
+        a1 = rr_reduce_q(rr_sub_nc<16>(s0, s1));
+        b0 = rr_carry_seq(rr_add_nc(d0, d1));
+        b1 = rr_reduce_q(rr_sub_nc<4>(d0, d1));
+      }
+      U.put(j, a0);
+      U.put(j + h, a1);
+      U.put(j + bit, b0);
+      U.put(j + bit + h, b1);
+    }
+    __syncthreads();
+  }
+  if (r < DEG) {  // odd DEG: last radix-2 round (bit = 1, trivial twiddles)
+    for (uint32_t f = threadIdx.x; f < E / 2; f += blockDim.x) {
+      const uint32_t i0 = 2 * f;
+      const F u0 = U.get(i0), u1 = U.get(i0 + 1);
+      U.put(i0, rr_reduce_q(rr_add_nc(u0, u1)));
+      U.put(i0 + 1, rr_reduce_q(rr_sub_nc<8>(u0, u1)));
+    }
+    __syncthreads();
+  }
+
+  // ---- store: y[(g - k) 2^DEG + k + j 2^lgp] = v[j] (natural order)
+  {
+    const uint64_t p = 1ull << lgp;
+    const uint32_t lpp = lgp < log_g ? lgp : log_g;
+    const uint32_t pp = 1u << lpp;
+#pragma unroll
+    for (int q = 0; q < NTT_EPT; q++) {
+      const uint32_t f = threadIdx.x + q * blockDim.x;
+      if (f >= E) break;
+      const uint32_t kk = f & (pp - 1);
+      const uint32_t jj = (f >> lpp) & (R - 1);
+      const uint32_t gh = f >> (lpp + DEG);
+      const uint32_t gi = (gh << lpp) + kk;
+      const uint64_t g = g0 + gi;
+      const uint64_t k = g & (p - 1);
+      const size_t dst = ((g - k) << DEG) + k + (uint64_t)jj * p;
+      const F v = U.get((gi << DEG) + bitrev(jj, DEG));
+      rr_store_std<Q>(y, dst, v);
+    }
+  }
+}
+
+// boundary-form table entries w R -> w R' (canonical, packed in 8 words)
+template <class Q>
+__global__ void ntt_tab_to_rr_kernel(const Fp<typename Q::Base>* __restrict__ in, uint64_t cnt,
+                                     uint4* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cnt) return;
+  rr_store_std<Q>(out, i, rr_from_std<Q>(load(&in[i])));
+}
+
 // Full inter-pass twiddle table of one pass: out[i * p + k] = w^((k i) << s),
 // i < 2^deg, k < p = 2^lgp, s = log n - lgp - deg.
 template <class P>
@@ -308,6 +522,57 @@ static hipError_t launch_pass(const PassArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <class Q, int DEG>
+static hipError_t launch_pass_rr(const PassArgs& a, const void* pq, const void* twf, hipStream_t s) {
+  const uint32_t tile_log = DEG > ntt_tile_log() ? DEG : ntt_tile_log();
+  uint32_t log_g = tile_log - DEG;
+  const uint32_t log_groups = a.log_n - DEG;
+  if (log_g > log_groups) log_g = log_groups;
+  const uint32_t E = 1u << (DEG + log_g);
+  const uint64_t blocks = 1ull << (log_groups - log_g);
+  const size_t lds = (size_t)E * 36;  // three planes: 16 + 16 + 4 B per element
+  uint32_t threads = E / NTT_EPT;
+  if (threads < 64) threads = 64;
+  if (threads > NTT_RR_THREADS) return hipErrorInvalidValue;  // tiles of <= 1024 elements only
+  auto kern = ntt_pass_rr_kernel<Q, DEG>;
+  static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(threads), lds, s, (const uint4*)a.x, (uint4*)a.y,
+                     (const uint4*)pq, a.pq_shift, (const uint4*)twf, a.log_n, a.lgp, log_g);
+  return hipGetLastError();
+}
+
+template <class Q>
+static hipError_t launch_pass_rr_deg(int deg, const PassArgs& a, const void* pq, const void* twf, hipStream_t s) {
+  switch (deg) {
+    case 1: return launch_pass_rr<Q, 1>(a, pq, twf, s);
+    case 2: return launch_pass_rr<Q, 2>(a, pq, twf, s);
+    case 3: return launch_pass_rr<Q, 3>(a, pq, twf, s);
+    case 4: return launch_pass_rr<Q, 4>(a, pq, twf, s);
+    case 5: return launch_pass_rr<Q, 5>(a, pq, twf, s);
+    case 6: return launch_pass_rr<Q, 6>(a, pq, twf, s);
+    case 7: return launch_pass_rr<Q, 7>(a, pq, twf, s);
+    case 8: return launch_pass_rr<Q, 8>(a, pq, twf, s);
+    case 9: return launch_pass_rr<Q, 9>(a, pq, twf, s);
+    case 10: return launch_pass_rr<Q, 10>(a, pq, twf, s);
+    case 11: return launch_pass_rr<Q, 11>(a, pq, twf, s);
+    case 12: return launch_pass_rr<Q, 12>(a, pq, twf, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+static bool ntt_rr_enabled() {  // reduced-radix butterflies (A/B: ECG_NTT_RR=0 keeps the 32-bit-limb passes)
+  static bool v = [] {
+    const char* e = getenv("ECG_NTT_RR");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <class P, bool V1>
 static hipError_t launch_pass_deg(int deg, const PassArgs& a, hipStream_t s) {
   switch (deg) {
@@ -370,7 +635,7 @@ static int plan_passes(uint32_t log_n, int variant, uint32_t* degs) {
   return np;
 }
 
-template <class P>
+template <class P, class Q>
 static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uint32_t log_n,
                      hipStream_t s, ecg_abort_cb abort_cb, void* user) {
   using F = Fp<P>;
@@ -385,41 +650,52 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
   const uint64_t hi_cnt = n > lo_cnt ? (n >> NTT_LO_BITS) : 1;
   const uint64_t pq_cnt = max_deg > 1 ? 1ull << (max_deg - 1) : 1;
 
+  // full per-pass tables (passes after the first): sum of 2^(lgp + deg) <= 2n entries
+  const bool full = ntt_full_twiddles() && log_n <= 28 && np > 1;
+  // reduced-radix passes need the full tables (their twiddles are one load each)
+  const bool rr = ntt_rr_enabled() && variant == 2 && (np == 1 || full) && (1u << (max_deg > ntt_tile_log() ? max_deg : ntt_tile_log())) <= 4 * NTT_RR_THREADS;
+  const size_t elem = sizeof(F);  // bytes per element between passes (both forms)
+
   void *scratch = nullptr, *scratch2 = nullptr, *tables;
-  if (np > 1 || variant == 1) ECG_TRY(ws_get(ctx, "ntt_scratch", n * sizeof(F), &scratch));
+  if (np > 1 || variant == 1) ECG_TRY(ws_get(ctx, "ntt_scratch", n * elem, &scratch));
   // odd pass counts (> 1) rotate through a second scratch buffer so the last
   // pass writes d_data directly (no copy back; HBM is plentiful)
-  if (np > 1 && (np & 1)) ECG_TRY(ws_get(ctx, "ntt_scratch2", n * sizeof(F), &scratch2));
+  if (np > 1 && (np & 1)) ECG_TRY(ws_get(ctx, "ntt_scratch2", n * elem, &scratch2));
   ECG_TRY(ws_get(ctx, "ntt_tables", (pq_cnt + lo_cnt + hi_cnt) * sizeof(F), &tables));
   F* pq = (F*)tables;
   F* tw_lo = pq + pq_cnt;
   F* tw_hi = tw_lo + lo_cnt;
 
-  // full per-pass tables (passes after the first): sum of 2^(lgp + deg) <= 2n entries
-  const bool full = ntt_full_twiddles() && log_n <= 28 && np > 1;
   F* twf[40] = {nullptr};
+  uint64_t twf_off[40] = {0}, twf_tot = 0;
   if (full) {
-    uint64_t tot = 0;
     uint32_t lg = 0;
     for (int k = 0; k < np; k++) {
-      if (k > 0) tot += 1ull << (lg + degs[k]);
+      if (k > 0) {
+        twf_off[k] = twf_tot;
+        twf_tot += 1ull << (lg + degs[k]);
+      }
       lg += degs[k];
     }
     void* t;
-    ECG_TRY(ws_get(ctx, "ntt_twf", tot * sizeof(F), &t));
-    uint64_t off = 0;
-    lg = 0;
-    for (int k = 0; k < np; k++) {
-      if (k > 0) {
-        twf[k] = (F*)t + off;
-        off += 1ull << (lg + degs[k]);
-      }
-      lg += degs[k];
+    ECG_TRY(ws_get(ctx, "ntt_twf", twf_tot * sizeof(F), &t));
+    for (int k = 1; k < np; k++) twf[k] = (F*)t + twf_off[k];
+  }
+  // the reduced-radix passes' twiddles: w R' (canonical, packed)
+  F *pq_rr = nullptr, *twf_rr = nullptr;
+  if (rr) {
+    void *a, *b;
+    ECG_TRY(ws_get(ctx, "ntt_pq_rr", pq_cnt * sizeof(F), &a));
+    pq_rr = (F*)a;
+    if (full) {
+      ECG_TRY(ws_get(ctx, "ntt_twf_rr", twf_tot * sizeof(F), &b));
+      twf_rr = (F*)b;
     }
   }
 
   const bool cached = ctx->tw_fid == field_id && ctx->tw_log_n == log_n && ctx->tw_variant == variant &&
-                      ctx->tw_full == (int)full && memcmp(ctx->tw_omega, omega, sizeof(ctx->tw_omega)) == 0;
+                      ctx->tw_full == (int)full + 2 * (int)rr &&
+                      memcmp(ctx->tw_omega, omega, sizeof(ctx->tw_omega)) == 0;
   if (!cached) {
     F w;
     memcpy(w.v, omega, sizeof(w.v));
@@ -441,11 +717,18 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
         lg += degs[k];
       }
     }
+    if (rr) {
+      hipLaunchKernelGGL(ntt_tab_to_rr_kernel<Q>, dim3((uint32_t)((pq_cnt + 255) / 256)), dim3(256), 0, s, pq,
+                         pq_cnt, (uint4*)pq_rr);
+      if (full)
+        hipLaunchKernelGGL(ntt_tab_to_rr_kernel<Q>, dim3((uint32_t)((twf_tot + 255) / 256)), dim3(256), 0, s,
+                           twf[1], twf_tot, (uint4*)twf_rr);
+    }
     ECG_HIP(hipGetLastError());
     ctx->tw_fid = field_id;
     ctx->tw_log_n = log_n;
     ctx->tw_variant = variant;
-    ctx->tw_full = (int)full;
+    ctx->tw_full = (int)full + 2 * (int)rr;
     memcpy(ctx->tw_omega, omega, sizeof(ctx->tw_omega));
   }
 
@@ -453,7 +736,6 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
   // Single-pass v2 transforms (log n <= 12) have one workgroup reading every
   // element before any write: safe in place.  Otherwise ping-pong, arranged so
   // the last pass lands in d_data whenever the pass count is even.
-  // buffer sequence: d_data -> ... -> d_data
   void* bufs[41];
   bufs[0] = d_data;
   for (int k = 1; k <= np; k++) {
@@ -463,17 +745,16 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
     else if (np & 1) bufs[k] = (k & 1) ? scratch : scratch2;       // odd: rotate two scratches
     else bufs[k] = (k & 1) ? scratch : d_data;                     // even: ping-pong
   }
-  void* src = d_data;
-  void* dst = bufs[1];
   uint32_t lgp = 0;
   for (int k = 0; k < np; k++) {
     if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // fft.rs:94-98
-    src = bufs[k];
-    dst = bufs[k + 1];
-    const PassArgs a{src, dst, pq, max_deg - degs[k], tw_lo, tw_hi, twf[k], log_n, lgp};
+    const PassArgs a{bufs[k], bufs[k + 1], pq, max_deg - degs[k], tw_lo, tw_hi, twf[k], log_n, lgp};
     ECG_TRY(kt_begin(ctx, "ntt_pass", s));
-    hipError_t e = variant == 1 ? launch_pass_deg<P, true>((int)degs[k], a, s)
-                                : launch_pass_deg<P, false>((int)degs[k], a, s);
+    hipError_t e;
+    if (rr)
+      e = launch_pass_rr_deg<Q>((int)degs[k], a, pq_rr, k > 0 ? twf_rr + twf_off[k] : nullptr, s);
+    else
+      e = variant == 1 ? launch_pass_deg<P, true>((int)degs[k], a, s) : launch_pass_deg<P, false>((int)degs[k], a, s);
     ECG_HIP(e);
     ECG_TRY(kt_end(ctx, "ntt_pass", s));
     lgp += degs[k];
@@ -507,9 +788,11 @@ int ntt_run(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uin
   ECG_TRY(ntt_validate(field_id, log_n));
   switch (field_id) {
     case ECG_FIELD_BLS12_381_FR:
-      return ntt_run_t<params::bls12_381_fr>(ctx, field_id, d_data, omega, log_n, s, abort_cb, user);
+      return ntt_run_t<params::bls12_381_fr, params::bls12_381_fr_rr>(ctx, field_id, d_data, omega, log_n, s,
+                                                                       abort_cb, user);
     default:
-      return ntt_run_t<params::bn254_fr>(ctx, field_id, d_data, omega, log_n, s, abort_cb, user);
+      return ntt_run_t<params::bn254_fr, params::bn254_fr_rr>(ctx, field_id, d_data, omega, log_n, s, abort_cb,
+                                                               user);
   }
 }
 
