@@ -83,10 +83,11 @@ template <class Q>
 ECG_DEV XYZZ<FpR<Q>> rr_add_affine(const XYZZ<FpR<Q>>& p, const Affine<FpR<Q>>& a) {
   using F = FpR<Q>;
   XYZZ<F> r;
-  const F ay = rr_carry<Q>(a.y.v);  // stored points are QN
+  // a.y (possibly wide) is carried only where it becomes a stored coordinate
+  // (stored points are QN); the common path feeds it straight into a product
   if (xyzz_is_zero_rr(p)) {
     r.X = a.x;
-    r.Y = ay;
+    r.Y = rr_carry<Q>(a.y.v);
     r.ZZ = F::one();
     r.ZZZ = F::one();
   } else {
@@ -106,7 +107,7 @@ ECG_DEV XYZZ<FpR<Q>> rr_add_affine(const XYZZ<FpR<Q>>& p, const Affine<FpR<Q>>& 
       if (dbl) {
         Affine<F> b;
         b.x = a.x;
-        b.y = ay;
+        b.y = rr_carry<Q>(a.y.v);
         d = rr_dbl_affine(b);
       }
       rr_sel(r, inf, d);

@@ -189,29 +189,91 @@ ECG_DEV void mad64x8s(uint64_t& acc0, const uint32_t* m0, uint64_t& acc1, const 
         "s"(u[0]), "s"(u[1]), "s"(u[2]), "s"(u[3]));
 }
 
+// First products of a column: the same pairs with a zero addend for chain 0
+// (Z0) and/or chain 1 (Z1), which starts that accumulator instead of a
+// v_mov_b64 of 0 ahead of the column.
+template <bool Z0, bool Z1>
+ECG_DEV void mad64x2_z(uint64_t& acc0, uint32_t a0, uint32_t b0, uint64_t& acc1, uint32_t a1, uint32_t b1) {
+  uint64_t c0, c1;
+  if constexpr (Z0 && Z1)
+    asm("v_mad_u64_u32 %0, %2, %4, %5, 0\n\t"
+        "v_mad_u64_u32 %1, %3, %6, %7, 0"
+        : "=&v"(acc0), "=&v"(acc1), "=&s"(c0), "=&s"(c1)
+        : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+  else if constexpr (Z1)
+    asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+        "v_mad_u64_u32 %1, %3, %6, %7, 0"
+        : "+v"(acc0), "=&v"(acc1), "=&s"(c0), "=&s"(c1)
+        : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+  else
+    mad64x2(acc0, a0, b0, acc1, a1, b1);
+}
+// acc0 += a0 b0 + c0 d0; acc1 = a1 b1 + c1 d1 (chain 1 starts at zero)
+ECG_DEV void mad64x4_z1(uint64_t& acc0, uint32_t a0, uint32_t b0, uint32_t c0, uint32_t d0, uint64_t& acc1,
+                        uint32_t a1, uint32_t b1, uint32_t c1, uint32_t d1) {
+  uint64_t k0, k1;
+  asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %8, %9, 0\n\t"
+      "v_mad_u64_u32 %0, %2, %6, %7, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %10, %11, %1"
+      : "+v"(acc0), "=&v"(acc1), "=&s"(k0), "=&s"(k1)
+      : "v"(a0), "v"(b0), "v"(c0), "v"(d0), "v"(a1), "v"(b1), "v"(c1), "v"(d1));
+}
+// mad64x8 with chain 1 starting at zero
+ECG_DEV void mad64x8_z1(uint64_t& acc0, const uint32_t* a0, const uint32_t* b0, uint64_t& acc1, const uint32_t* a1,
+                        const uint32_t* b1) {
+  uint64_t k0, k1;
+  asm("v_mad_u64_u32 %0, %2, %4, %5, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %12, %13, 0\n\t"
+      "v_mad_u64_u32 %0, %2, %6, %7, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %14, %15, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %8, %9, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %16, %17, %1\n\t"
+      "v_mad_u64_u32 %0, %2, %10, %11, %0\n\t"
+      "v_mad_u64_u32 %1, %3, %18, %19, %1"
+      : "+v"(acc0), "=&v"(acc1), "=&s"(k0), "=&s"(k1)
+      : "v"(a0[0]), "v"(b0[0]), "v"(a0[1]), "v"(b0[1]), "v"(a0[2]), "v"(b0[2]), "v"(a0[3]), "v"(b0[3]),
+        "v"(a1[0]), "v"(b1[0]), "v"(a1[1]), "v"(b1[1]), "v"(a1[2]), "v"(b1[2]), "v"(a1[3]), "v"(b1[3]));
+}
+
 // Column pieces of two interleaved products (k, lo, hi fold to constants in
 // the unrolled column loops): sum_{lo <= i <= hi} a_i b_{k-i} into (x0, x1),
 // and sum_{lo <= i <= hi} m_i P_{k-i} for the uniform modulus limbs P.
+// Z1: chain 1 starts at zero with the column's first statement (lo <= hi).
+template <bool Z1 = false>
 ECG_DEV void col2(int k, int lo, int hi, uint64_t& x0, const uint32_t* a0, const uint32_t* b0, uint64_t& x1,
                   const uint32_t* a1, const uint32_t* b1) {
+  bool first = Z1;
 #if !defined(ECG_RR_NO_X4) && !defined(ECG_RR_X4_ONLY)
   for (; lo + 3 <= hi; lo += 4) {
     const uint32_t ta0[4] = {a0[lo], a0[lo + 1], a0[lo + 2], a0[lo + 3]};
     const uint32_t tb0[4] = {b0[k - lo], b0[k - lo - 1], b0[k - lo - 2], b0[k - lo - 3]};
     const uint32_t ta1[4] = {a1[lo], a1[lo + 1], a1[lo + 2], a1[lo + 3]};
     const uint32_t tb1[4] = {b1[k - lo], b1[k - lo - 1], b1[k - lo - 2], b1[k - lo - 3]};
-    mad64x8(x0, ta0, tb0, x1, ta1, tb1);
+    if (first)
+      mad64x8_z1(x0, ta0, tb0, x1, ta1, tb1);
+    else
+      mad64x8(x0, ta0, tb0, x1, ta1, tb1);
+    first = false;
   }
 #endif
 #pragma unroll
   for (int i = lo; i <= hi; i += 2) {
 #ifndef ECG_RR_NO_X4
     if (i + 1 <= hi) {
-      mad64x4(x0, a0[i], b0[k - i], a0[i + 1], b0[k - i - 1], x1, a1[i], b1[k - i], a1[i + 1], b1[k - i - 1]);
+      if (first)
+        mad64x4_z1(x0, a0[i], b0[k - i], a0[i + 1], b0[k - i - 1], x1, a1[i], b1[k - i], a1[i + 1], b1[k - i - 1]);
+      else
+        mad64x4(x0, a0[i], b0[k - i], a0[i + 1], b0[k - i - 1], x1, a1[i], b1[k - i], a1[i + 1], b1[k - i - 1]);
+      first = false;
       continue;
     }
 #endif
-    mad64x2(x0, a0[i], b0[k - i], x1, a1[i], b1[k - i]);
+    if (first)
+      mad64x2_z<false, true>(x0, a0[i], b0[k - i], x1, a1[i], b1[k - i]);
+    else
+      mad64x2(x0, a0[i], b0[k - i], x1, a1[i], b1[k - i]);
+    first = false;
 #ifdef ECG_RR_NO_X4
     if (i + 1 <= hi) mad64x2(x0, a0[i + 1], b0[k - i - 1], x1, a1[i + 1], b1[k - i - 1]);
 #endif
@@ -249,10 +311,11 @@ ECG_DEV void rr_mul2(const FpR<Q>& a0, const FpR<Q>& b0, const FpR<Q>& a1, const
   constexpr int NL = Q::NL, B = Q::BITS;
   constexpr uint32_t MASK = (1u << B) - 1;
   uint32_t m0[NL], m1[NL];
-  uint64_t x0 = 0, x1 = 0;
+  uint64_t x0, x1;
+  mad64x2_z<true, true>(x0, a0.v[0], b0.v[0], x1, a1.v[0], b1.v[0]);  // column 0 starts both chains
 #pragma unroll
   for (int k = 0; k < NL; k++) {
-    col2(k, 0, k, x0, a0.v, b0.v, x1, a1.v, b1.v);
+    if (k > 0) col2(k, 0, k, x0, a0.v, b0.v, x1, a1.v, b1.v);
     col2p<Q>(k, 0, k - 1, x0, m0, x1, m1);
     m0[k] = ((uint32_t)x0 * Q::INV) & MASK;
     m1[k] = ((uint32_t)x1 * Q::INV) & MASK;
@@ -292,19 +355,21 @@ ECG_DEV FpR<Q> rr_mul_sum2(const FpR<Q>& a, const FpR<Q>& b, const FpR<Q>& c, co
   constexpr uint32_t MASK = (1u << B) - 1;
   uint32_t m[NL];
   FpR<Q> r;
-  uint64_t x0 = 0, x1 = 0;
+  uint64_t x0, x1;
 #pragma unroll
   for (int k = 0; k < 2 * NL - 1; k++) {
     const int i0 = k < NL ? 0 : k - NL + 1;
     const int i1 = k < NL ? k : NL - 1;
-    col2(k, i0, i1, x0, a.v, b.v, x1, c.v, d.v);
+    if (k == 0)  // both chains start at zero
+      mad64x2_z<true, true>(x0, a.v[0], b.v[0], x1, c.v[0], d.v[0]);
+    else  // chain 1 restarts at zero in every column
+      col2<true>(k, i0, i1, x0, a.v, b.v, x1, c.v, d.v);
     const int j1 = k < NL ? k - 1 : NL - 1;  // m[j] p[k-j], j in [i0, j1]
     int j = i0;
 #pragma unroll
     for (; j + 1 <= j1; j += 2) mad64x2ss(x0, m[j], Q::P[k - j], x1, m[j + 1], Q::P[k - j - 1]);
     if (j == j1) mad64s(x0, m[j], Q::P[k - j]);
     x0 += x1;
-    x1 = 0;
     if (k < NL) {
       m[k] = ((uint32_t)x0 * Q::INV) & MASK;
       mad64s(x0, m[k], Q::P[0]);
@@ -328,12 +393,15 @@ ECG_DEV void rr_sqr2(const FpR<Q>& a0, const FpR<Q>& a1, FpR<Q>& r0, FpR<Q>& r1)
     d0[i] = a0.v[i] + a0.v[i];
     d1[i] = a1.v[i] + a1.v[i];
   }
-  uint64_t x0 = 0, x1 = 0;
+  uint64_t x0, x1;
 #pragma unroll
   for (int k = 0; k < 2 * NL - 1; k++) {
     const int i0 = k < NL ? 0 : k - NL + 1;
     col2(k, i0, (k & 1) ? k / 2 : k / 2 - 1, x0, d0, a0.v, x1, d1, a1.v);  // 2 i < k
-    if ((k & 1) == 0) mad64x2(x0, a0.v[k >> 1], a0.v[k >> 1], x1, a1.v[k >> 1], a1.v[k >> 1]);
+    if (k == 0)  // column 0 (no off-diagonal term) starts both chains
+      mad64x2_z<true, true>(x0, a0.v[0], a0.v[0], x1, a1.v[0], a1.v[0]);
+    else if ((k & 1) == 0)
+      mad64x2(x0, a0.v[k >> 1], a0.v[k >> 1], x1, a1.v[k >> 1], a1.v[k >> 1]);
     if (k < NL) {
       col2p<Q>(k, 0, k - 1, x0, m0, x1, m1);
       m0[k] = ((uint32_t)x0 * Q::INV) & MASK;

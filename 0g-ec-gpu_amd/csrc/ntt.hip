@@ -253,11 +253,15 @@ __global__ void __launch_bounds__(256)
 //   b0 = carry(d0 + d1)                         (<= 2.3 r)
 //   b1 = (d0 + 4r - d1) w2                      (<= 1.1 r)
 // The last step of a pass (h = 1: three of its four twiddles are 1) uses
-// reduce_q instead of those three products.  In HBM -- pass inputs, outputs
-// and the twiddle tables -- every value is canonical (< r) and packed into
-// the 8-word boundary layout, so the strided Stockham gathers read whole
-// 128-B lines as the 32-bit-limb passes do; the 9-limb form lives only in
-// VGPRs and LDS.
+// reduce_q instead of those three products.
+//
+// HBM layout: the transform's input and output are the boundary layout
+// (canonical, 8 packed words).  Between passes the elements stay in the
+// E-form as three planes (limbs 0-3 | 4-7 | 8: 36 B per element, coalesced
+// 16-B / 4-B accesses), so an inner pass boundary costs no unpacking,
+// reduction, canonicalisation or packing (~125 VALU instructions per element
+// saved for 4 more bytes).  The twiddle tables are planes of exact canonical
+// limbs for the same reason.
 // ---------------------------------------------------------------------------
 template <class Q>
 struct RrPlanes {  // limbs 0-3 | 4-7 | 8 of element i (NL = 9)
@@ -284,6 +288,7 @@ struct RrPlanes {  // limbs 0-3 | 4-7 | 8 of element i (NL = 9)
     c[i] = v.v[8];
   }
 };
+constexpr size_t RR_PLANE_BYTES = 36;  // bytes per element in the plane layout
 
 template <class Q>
 ECG_DEV FpR<Q> rr_load_std(const uint4* __restrict__ x, size_t i) {  // 8 words x R -> 9 exact limbs
@@ -303,6 +308,15 @@ ECG_DEV void rr_store_std(uint4* __restrict__ y, size_t i, const FpR<Q>& v) {  /
   y[2 * i + 1] = make_uint4(w[4], w[5], w[6], w[7]);
 }
 
+// LDS layout: the three planes, unswizzled.  A linear XOR swizzle of the
+// element slots (found by a bank simulation of every access pattern of the
+// 1024-element tiles) cut SQ_LDS_BANK_CONFLICT from 1354 to 96 cycles per wave
+// but left the pass time unchanged and added ~3% VALU instructions for the
+// slot arithmetic: the pass is VALU-issue-bound (SQ_INSTS_VALU x 4 cycles ~
+// 0.94 of the wave cycles at 4 waves/SIMD), not LDS-bound
+// (profiles/r02b/ntt_lds_swizzle.txt).
+ECG_HD constexpr uint32_t lds_phys(uint32_t j) { return j; }
+
 // 256-thread workgroups (tiles of <= 1024 elements): at the 1024-thread bound
 // (128 VGPRs) the products spilled
 constexpr uint32_t NTT_RR_THREADS = 512;
@@ -310,11 +324,13 @@ constexpr uint32_t NTT_RR_THREADS = 512;
 #ifndef ECG_NTT_RR_WAVES
 #define ECG_NTT_RR_WAVES 4
 #endif
-template <class Q, int DEG>
+// IN_RR / OUT_RR: the pass reads / writes the plane layout (inner pass
+// boundaries) instead of the boundary layout.
+template <class Q, int DEG, bool IN_RR, bool OUT_RR>
 __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_per_eu(ECG_NTT_RR_WAVES)))
-    ntt_pass_rr_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, const uint4* __restrict__ pq,
-                       uint32_t pq_shift, const uint4* __restrict__ twf, uint32_t log_n, uint32_t lgp,
-                       uint32_t log_g) {
+    ntt_pass_rr_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, const uint4* __restrict__ pq_base,
+                       uint32_t pq_cnt, uint32_t pq_shift, const uint4* __restrict__ twf_base, uint64_t twf_cnt,
+                       uint64_t twf_off, uint32_t log_n, uint32_t lgp, uint32_t log_g) {
   using F = FpR<Q>;
   constexpr uint32_t R = 1u << DEG;
   extern __shared__ uint4 smem[];
@@ -323,6 +339,7 @@ __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_pe
   const uint32_t G = 1u << log_g;
   const size_t n = (size_t)1 << log_n;
   const uint64_t g0 = (uint64_t)blockIdx.x << log_g;
+  const RrPlanes<Q> PQ = RrPlanes<Q>::over(const_cast<uint4*>(pq_base), pq_cnt);
 
   // ---- load: u[i] = x[g + i t] * w^((n >> (lgp + DEG)) k i) (full per-pass table)
   {
@@ -335,16 +352,20 @@ __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_pe
       v[q] = F::zero();
       if (f < E) {
         const uint64_t src = g0 + (f & (G - 1)) + (uint64_t)(f >> log_g) * t;
-        v[q] = rr_load_std<Q>(x, src);
+        if constexpr (IN_RR)
+          v[q] = RrPlanes<Q>::over(const_cast<uint4*>(x), n).get(src);
+        else
+          v[q] = rr_load_std<Q>(x, src);
       }
     }
     if (lgp != 0) {  // every element times its twiddle (w^0 = 1 is a table entry too: no divergence)
+      const RrPlanes<Q> TW = RrPlanes<Q>::over(const_cast<uint4*>(twf_base), twf_cnt).at(twf_off);
       F w[NTT_EPT];
 #pragma unroll
       for (int q = 0; q < NTT_EPT; q++) {
         const uint32_t f = threadIdx.x + q * blockDim.x;
         const uint64_t g = g0 + (f & (G - 1));
-        w[q] = f < E ? rr_load_std<Q>(twf, (uint64_t)(f >> log_g) * p + (g & (p - 1))) : F::one();
+        w[q] = f < E ? TW.get((uint64_t)(f >> log_g) * p + (g & (p - 1))) : F::one();
       }
 #pragma unroll
       for (int q = 0; q + 1 < NTT_EPT; q += 2) {
@@ -357,7 +378,7 @@ __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_pe
 #pragma unroll
     for (int q = 0; q < NTT_EPT; q++) {
       const uint32_t f = threadIdx.x + q * blockDim.x;
-      if (f < E) U.put(((f & (G - 1)) << DEG) + (f >> log_g), v[q]);
+      if (f < E) U.put(lds_phys(((f & (G - 1)) << DEG) + (f >> log_g)), v[q]);
     }
   }
   __syncthreads();
@@ -368,44 +389,47 @@ __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_pe
 #pragma unroll 1
   for (; r + 1 < DEG; r += 2) {
     const uint32_t bit = (R / 2) >> r, h = bit >> 1;
+    // slots of the quartet offsets h, bit, bit + h (disjoint from j's bits)
+    const uint32_t oh = lds_phys(h), ob = lds_phys(bit), obh = lds_phys(bit + h);
     for (uint32_t f = threadIdx.x; f < E / 4; f += blockDim.x) {
       const uint32_t gi = f / RQ, q = f % RQ;
       const uint32_t qm = q & (h - 1);
       const uint32_t j = (gi << DEG) + ((q / h) * (2 * bit)) + qm;
-      const F e0 = U.get(j), e1 = U.get(j + h), e2 = U.get(j + bit), e3 = U.get(j + bit + h);
+      const uint32_t pj = lds_phys(j);
+      const F e0 = U.get(pj), e1 = U.get(pj ^ oh), e2 = U.get(pj ^ ob), e3 = U.get(pj ^ obh);
       const F s0 = rr_add_nc(e0, e2), s1 = rr_add_nc(e1, e3);
       F a0, a1, b0, b1;
       if (h > 1) {
         F d0, d1, a1p, b1p;
-        rr_mul2(rr_sub_nc<8>(e0, e2), rr_load_std<Q>(pq, (size_t)(qm << r) << pq_shift), rr_sub_nc<8>(e1, e3),
-                rr_load_std<Q>(pq, (size_t)((qm + h) << r) << pq_shift), d0, d1);
+        rr_mul2(rr_sub_nc<8>(e0, e2), PQ.get((size_t)(qm << r) << pq_shift), rr_sub_nc<8>(e1, e3),
+                PQ.get((size_t)((qm + h) << r) << pq_shift), d0, d1);
         a0 = rr_reduce_q(rr_add_nc(s0, s1));
         b0 = rr_carry_seq(rr_add_nc(d0, d1));
-        const F w2 = rr_load_std<Q>(pq, (size_t)(qm << (r + 1)) << pq_shift);
+        const F w2 = PQ.get((size_t)(qm << (r + 1)) << pq_shift);
         rr_mul2(rr_sub_nc<16>(s0, s1), w2, rr_sub_nc<4>(d0, d1), w2, a1p, b1p);
         a1 = a1p;
         b1 = b1p;
       } else {  // h = 1: qm = 0, so d1's twiddle w^(1 << r) is the only non-trivial one
         const F d0 = rr_reduce_q(rr_sub_nc<8>(e0, e2));
-        const F d1 = rr_mul(rr_sub_nc<8>(e1, e3), rr_load_std<Q>(pq, (size_t)(1u << r) << pq_shift));
+        const F d1 = rr_mul(rr_sub_nc<8>(e1, e3), PQ.get((size_t)(1u << r) << pq_shift));
         a0 = rr_reduce_q(rr_add_nc(s0, s1));
         a1 = rr_reduce_q(rr_sub_nc<16>(s0, s1));
         b0 = rr_carry_seq(rr_add_nc(d0, d1));
         b1 = rr_reduce_q(rr_sub_nc<4>(d0, d1));
       }
-      U.put(j, a0);
-      U.put(j + h, a1);
-      U.put(j + bit, b0);
-      U.put(j + bit + h, b1);
+      U.put(pj, a0);
+      U.put(pj ^ oh, a1);
+      U.put(pj ^ ob, b0);
+      U.put(pj ^ obh, b1);
     }
     __syncthreads();
   }
   if (r < DEG) {  // odd DEG: last radix-2 round (bit = 1, trivial twiddles)
     for (uint32_t f = threadIdx.x; f < E / 2; f += blockDim.x) {
-      const uint32_t i0 = 2 * f;
-      const F u0 = U.get(i0), u1 = U.get(i0 + 1);
-      U.put(i0, rr_reduce_q(rr_add_nc(u0, u1)));
-      U.put(i0 + 1, rr_reduce_q(rr_sub_nc<8>(u0, u1)));
+      const uint32_t p0 = lds_phys(2 * f);  // phys(2f + 1) = phys(2f) ^ 1
+      const F u0 = U.get(p0), u1 = U.get(p0 ^ 1);
+      U.put(p0, rr_reduce_q(rr_add_nc(u0, u1)));
+      U.put(p0 ^ 1, rr_reduce_q(rr_sub_nc<8>(u0, u1)));
     }
     __syncthreads();
   }
@@ -426,19 +450,21 @@ __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_pe
       const uint64_t g = g0 + gi;
       const uint64_t k = g & (p - 1);
       const size_t dst = ((g - k) << DEG) + k + (uint64_t)jj * p;
-      const F v = U.get((gi << DEG) + bitrev(jj, DEG));
-      rr_store_std<Q>(y, dst, v);
+      const F v = U.get(lds_phys((gi << DEG) + bitrev(jj, DEG)));
+      if constexpr (OUT_RR)
+        RrPlanes<Q>::over(y, n).put(dst, v);  // E-form: the next pass multiplies it by its twiddle first
+      else
+        rr_store_std<Q>(y, dst, v);
     }
   }
 }
 
-// boundary-form table entries w R -> w R' (canonical, packed in 8 words)
+// boundary-form table entries w R -> w R' as planes of exact canonical limbs
 template <class Q>
-__global__ void ntt_tab_to_rr_kernel(const Fp<typename Q::Base>* __restrict__ in, uint64_t cnt,
-                                     uint4* __restrict__ out) {
+__global__ void ntt_tab_to_rr_kernel(const Fp<typename Q::Base>* __restrict__ in, uint64_t cnt, uint4* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cnt) return;
-  rr_store_std<Q>(out, i, rr_from_std<Q>(load(&in[i])));
+  RrPlanes<Q>::over(out, cnt).put(i, rr_canon_lt2p(rr_reduce_q(rr_from_std<Q>(load(&in[i])))));
 }
 
 // Full inter-pass twiddle table of one pass: out[i * p + k] = w^((k i) << s),
@@ -522,19 +548,28 @@ static hipError_t launch_pass(const PassArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <class Q, int DEG>
-static hipError_t launch_pass_rr(const PassArgs& a, const void* pq, const void* twf, hipStream_t s) {
+// Tables of the reduced-radix passes (planes): pq (cnt entries) and the full
+// per-pass twiddles (twf_cnt entries over all passes, this pass at twf_off).
+struct RrTables {
+  const void* pq;
+  uint32_t pq_cnt;
+  const void* twf;
+  uint64_t twf_cnt, twf_off;
+};
+
+template <class Q, int DEG, bool IN_RR, bool OUT_RR>
+static hipError_t launch_pass_rr(const PassArgs& a, const RrTables& t, hipStream_t s) {
   const uint32_t tile_log = DEG > ntt_tile_log() ? DEG : ntt_tile_log();
   uint32_t log_g = tile_log - DEG;
   const uint32_t log_groups = a.log_n - DEG;
   if (log_g > log_groups) log_g = log_groups;
   const uint32_t E = 1u << (DEG + log_g);
   const uint64_t blocks = 1ull << (log_groups - log_g);
-  const size_t lds = (size_t)E * 36;  // three planes: 16 + 16 + 4 B per element
+  const size_t lds = (size_t)E * RR_PLANE_BYTES;
   uint32_t threads = E / NTT_EPT;
   if (threads < 64) threads = 64;
-  if (threads > NTT_RR_THREADS) return hipErrorInvalidValue;  // tiles of <= 1024 elements only
-  auto kern = ntt_pass_rr_kernel<Q, DEG>;
+  if (threads > NTT_RR_THREADS) return hipErrorInvalidValue;  // tiles of <= 2048 elements only
+  auto kern = ntt_pass_rr_kernel<Q, DEG, IN_RR, OUT_RR>;
   static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -542,25 +577,32 @@ static hipError_t launch_pass_rr(const PassArgs& a, const void* pq, const void* 
     attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(threads), lds, s, (const uint4*)a.x, (uint4*)a.y,
-                     (const uint4*)pq, a.pq_shift, (const uint4*)twf, a.log_n, a.lgp, log_g);
+                     (const uint4*)t.pq, t.pq_cnt, a.pq_shift, (const uint4*)t.twf, t.twf_cnt, t.twf_off, a.log_n,
+                     a.lgp, log_g);
   return hipGetLastError();
 }
 
+template <class Q, int DEG>
+static hipError_t launch_pass_rr_io(bool in_rr, bool out_rr, const PassArgs& a, const RrTables& t, hipStream_t s) {
+  if (in_rr) return out_rr ? launch_pass_rr<Q, DEG, true, true>(a, t, s) : launch_pass_rr<Q, DEG, true, false>(a, t, s);
+  return out_rr ? launch_pass_rr<Q, DEG, false, true>(a, t, s) : launch_pass_rr<Q, DEG, false, false>(a, t, s);
+}
+
 template <class Q>
-static hipError_t launch_pass_rr_deg(int deg, const PassArgs& a, const void* pq, const void* twf, hipStream_t s) {
+static hipError_t launch_pass_rr_deg(int deg, bool in_rr, bool out_rr, const PassArgs& a, const RrTables& t,
+                                     hipStream_t s) {
   switch (deg) {
-    case 1: return launch_pass_rr<Q, 1>(a, pq, twf, s);
-    case 2: return launch_pass_rr<Q, 2>(a, pq, twf, s);
-    case 3: return launch_pass_rr<Q, 3>(a, pq, twf, s);
-    case 4: return launch_pass_rr<Q, 4>(a, pq, twf, s);
-    case 5: return launch_pass_rr<Q, 5>(a, pq, twf, s);
-    case 6: return launch_pass_rr<Q, 6>(a, pq, twf, s);
-    case 7: return launch_pass_rr<Q, 7>(a, pq, twf, s);
-    case 8: return launch_pass_rr<Q, 8>(a, pq, twf, s);
-    case 9: return launch_pass_rr<Q, 9>(a, pq, twf, s);
-    case 10: return launch_pass_rr<Q, 10>(a, pq, twf, s);
-    case 11: return launch_pass_rr<Q, 11>(a, pq, twf, s);
-    case 12: return launch_pass_rr<Q, 12>(a, pq, twf, s);
+    case 1: return launch_pass_rr_io<Q, 1>(in_rr, out_rr, a, t, s);
+    case 2: return launch_pass_rr_io<Q, 2>(in_rr, out_rr, a, t, s);
+    case 3: return launch_pass_rr_io<Q, 3>(in_rr, out_rr, a, t, s);
+    case 4: return launch_pass_rr_io<Q, 4>(in_rr, out_rr, a, t, s);
+    case 5: return launch_pass_rr_io<Q, 5>(in_rr, out_rr, a, t, s);
+    case 6: return launch_pass_rr_io<Q, 6>(in_rr, out_rr, a, t, s);
+    case 7: return launch_pass_rr_io<Q, 7>(in_rr, out_rr, a, t, s);
+    case 8: return launch_pass_rr_io<Q, 8>(in_rr, out_rr, a, t, s);
+    case 9: return launch_pass_rr_io<Q, 9>(in_rr, out_rr, a, t, s);
+    case 10: return launch_pass_rr_io<Q, 10>(in_rr, out_rr, a, t, s);
+    case 11: return launch_pass_rr_io<Q, 11>(in_rr, out_rr, a, t, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -654,13 +696,16 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
   const bool full = ntt_full_twiddles() && log_n <= 28 && np > 1;
   // reduced-radix passes need the full tables (their twiddles are one load each)
   const bool rr = ntt_rr_enabled() && variant == 2 && (np == 1 || full) && (1u << (max_deg > ntt_tile_log() ? max_deg : ntt_tile_log())) <= 4 * NTT_RR_THREADS;
-  const size_t elem = sizeof(F);  // bytes per element between passes (both forms)
+  // bytes per element between passes: the plane layout for the reduced-radix
+  // passes, the boundary layout otherwise
+  const size_t elem = rr ? RR_PLANE_BYTES : sizeof(F);
 
   void *scratch = nullptr, *scratch2 = nullptr, *tables;
   if (np > 1 || variant == 1) ECG_TRY(ws_get(ctx, "ntt_scratch", n * elem, &scratch));
   // odd pass counts (> 1) rotate through a second scratch buffer so the last
-  // pass writes d_data directly (no copy back; HBM is plentiful)
-  if (np > 1 && (np & 1)) ECG_TRY(ws_get(ctx, "ntt_scratch2", n * elem, &scratch2));
+  // pass writes d_data directly (no copy back; HBM is plentiful); the
+  // reduced-radix inner passes always rotate two (planes do not fit d_data)
+  if (np > 1 && ((np & 1) || (rr && np > 2))) ECG_TRY(ws_get(ctx, "ntt_scratch2", n * elem, &scratch2));
   ECG_TRY(ws_get(ctx, "ntt_tables", (pq_cnt + lo_cnt + hi_cnt) * sizeof(F), &tables));
   F* pq = (F*)tables;
   F* tw_lo = pq + pq_cnt;
@@ -681,16 +726,11 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
     ECG_TRY(ws_get(ctx, "ntt_twf", twf_tot * sizeof(F), &t));
     for (int k = 1; k < np; k++) twf[k] = (F*)t + twf_off[k];
   }
-  // the reduced-radix passes' twiddles: w R' (canonical, packed)
-  F *pq_rr = nullptr, *twf_rr = nullptr;
+  // the reduced-radix passes' twiddles: w R' as planes of exact canonical limbs
+  void *pq_rr = nullptr, *twf_rr = nullptr;
   if (rr) {
-    void *a, *b;
-    ECG_TRY(ws_get(ctx, "ntt_pq_rr", pq_cnt * sizeof(F), &a));
-    pq_rr = (F*)a;
-    if (full) {
-      ECG_TRY(ws_get(ctx, "ntt_twf_rr", twf_tot * sizeof(F), &b));
-      twf_rr = (F*)b;
-    }
+    ECG_TRY(ws_get(ctx, "ntt_pq_rr", pq_cnt * RR_PLANE_BYTES, &pq_rr));
+    if (full) ECG_TRY(ws_get(ctx, "ntt_twf_rr", twf_tot * RR_PLANE_BYTES, &twf_rr));
   }
 
   const bool cached = ctx->tw_fid == field_id && ctx->tw_log_n == log_n && ctx->tw_variant == variant &&
@@ -742,6 +782,7 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
     if (variant == 1) bufs[k] = (k & 1) ? scratch : d_data;       // ping-pong + copy back (fft.rs:126)
     else if (np == 1) bufs[k] = d_data;                            // one workgroup: in place
     else if (k == np) bufs[k] = d_data;                            // last pass lands in place
+    else if (rr) bufs[k] = (k & 1) ? scratch : scratch2;           // planes: two scratches
     else if (np & 1) bufs[k] = (k & 1) ? scratch : scratch2;       // odd: rotate two scratches
     else bufs[k] = (k & 1) ? scratch : d_data;                     // even: ping-pong
   }
@@ -751,8 +792,10 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
     const PassArgs a{bufs[k], bufs[k + 1], pq, max_deg - degs[k], tw_lo, tw_hi, twf[k], log_n, lgp};
     ECG_TRY(kt_begin(ctx, "ntt_pass", s));
     hipError_t e;
-    if (rr)
-      e = launch_pass_rr_deg<Q>((int)degs[k], a, pq_rr, k > 0 ? twf_rr + twf_off[k] : nullptr, s);
+    if (rr) {
+      const RrTables t{pq_rr, (uint32_t)pq_cnt, twf_rr, twf_tot, twf_off[k]};
+      e = launch_pass_rr_deg<Q>((int)degs[k], k > 0, k + 1 < np, a, t, s);
+    }
     else
       e = variant == 1 ? launch_pass_deg<P, true>((int)degs[k], a, s) : launch_pass_deg<P, false>((int)degs[k], a, s);
     ECG_HIP(e);
