@@ -83,6 +83,13 @@ struct ecg_ctx {
     uint64_t fingerprint = 0;  // sampled host records at upload time
   };
   std::vector<BaseCache> base_cache;
+  // bases held in the bucket kernels' own layout (ecg_msm_prepare_bases,
+  // upload_multiexp_bases's role): prepared device pointer -> (curve, count)
+  struct Prepared {
+    int curve = -1;
+    size_t n = 0;
+  };
+  std::map<const void*, Prepared> prepared;
   // MSM terms per device pass (SingleMultiexpKernel::n, multiexp.rs:71-93);
   // 0 = derived from device memory (msm_chunk_terms)
   size_t msm_chunk = 0;
@@ -141,6 +148,9 @@ int dfft_run(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omega, u
 int comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes_per_peer, hipStream_t s);
 void comm_free(ecg_ctx* ctx);
 int comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes, hipStream_t s);
+// Bases [x, y] -> a new device buffer in the bucket kernels' layout,
+// registered in ctx->prepared (ecg_msm_prepare_bases).
+int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, void** d_out, hipStream_t s);
 int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const void* d_scalars,
                   int scalar_mont, size_t line_len, size_t n_chunks, uint32_t window_bits, uint64_t* out_jac,
                   hipStream_t s);

@@ -423,6 +423,24 @@ int ecg_msm_dev(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_s
   return kt_collect(ctx);
 }
 
+int ecg_msm_prepare_bases(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, void** d_prepared) {
+  ECG_ENTER(ctx);
+  if (!d_prepared || (!d_bases && n)) {
+    set_error("ecg_msm_prepare_bases: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  if (!curve_valid(curve_id)) {
+    set_error("prepare_bases: unknown curve_id %d", curve_id);
+    return ECG_ERR_INVALID;
+  }
+  if (n > 0x7fffffffull) {
+    set_error("prepare_bases: at most 2^31-1 bases");
+    return ECG_ERR_INVALID;
+  }
+  *d_prepared = nullptr;
+  return msm_prepare_run(ctx, curve_id, d_bases, n, d_prepared, ctx->stream);
+}
+
 int ecg_multiple_multiexp(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const uint64_t* scalars,
                           int scalars_on_device, int scalars_montgomery, size_t line_len, size_t num_chunks,
                           uint32_t window_bits, uint64_t* out_jac) {
@@ -617,8 +635,10 @@ int ecg_dev_alloc(ecg_ctx* ctx, size_t bytes, void** out) {
 
 void ecg_dev_free(ecg_ctx* ctx, void* p) {
   if (!ctx || !p) return;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  ctx->prepared.erase(p);  // a prepared-bases buffer is unregistered with its memory
   (void)hipFree(p);
 }
 

@@ -22,6 +22,22 @@ static const MsmOps* msm_ops(int curve_id, const char* what) {
   }
 }
 
+// Is d_bases a prepared buffer (ecg_msm_prepare_bases)?  It must then cover
+// the n bases the call reads, for the same curve.
+static int prepared_lookup(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, const char* what,
+                           bool* prepared) {
+  *prepared = false;
+  auto it = ctx->prepared.find(d_bases);
+  if (it == ctx->prepared.end()) return ECG_OK;
+  if (it->second.curve != curve_id || n > it->second.n) {
+    set_error("%s: prepared bases are %zu bases of curve %d, the call reads %zu of curve %d", what, it->second.n,
+              it->second.curve, n, curve_id);
+    return ECG_ERR_INVALID;
+  }
+  *prepared = true;
+  return ECG_OK;
+}
+
 int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
             hipStream_t s, ecg_abort_cb abort_cb, void* user, int scalar_mont) {
   if (n > 0x7fffffffull) {
@@ -30,7 +46,34 @@ int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scala
   }
   const MsmOps* o = msm_ops(curve_id, "multiexp");
   if (!o) return ECG_ERR_INVALID;
-  return o->single(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0);
+  bool prepared;
+  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n, "multiexp", &prepared));
+  return o->single(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0, prepared);
+}
+
+int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, void** d_out, hipStream_t s) {
+  const MsmOps* o = msm_ops(curve_id, "prepare_bases");
+  if (!o) return ECG_ERR_INVALID;
+  const size_t bytes = o->prepared_bytes(n);
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("prepare_bases: device allocation of %zu bytes failed: %s", bytes, hipGetErrorString(e));
+    return ECG_ERR_NOMEM;
+  }
+  int rc = o->prepare(ctx, d_bases, n, p, s);
+  if (rc == ECG_OK && hipStreamSynchronize(s) != hipSuccess) {
+    set_error("prepare_bases: %s", hipGetErrorString(hipGetLastError()));
+    rc = ECG_ERR_HIP;
+  }
+  if (rc != ECG_OK) {
+    (void)hipFree(p);
+    return rc;
+  }
+  ctx->prepared[p] = {curve_id, n};
+  *d_out = p;
+  return ECG_OK;
 }
 
 int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const void* d_scalars,
@@ -60,8 +103,10 @@ int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_base
   }
   const MsmOps* o = msm_ops(curve_id, "multiple_multiexp");
   if (!o) return ECG_ERR_INVALID;
+  bool prepared;
+  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n_bases, "multiple_multiexp", &prepared));
   return o->batch(ctx, d_bases, d_scalars, (uint32_t)n_lines, (uint32_t)n_chunks, line_len, scalar_mont != 0,
-                  window_bits, out_jac, s);
+                  window_bits, out_jac, s, prepared);
 }
 
 int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac) {

@@ -719,9 +719,11 @@ static inline uint32_t blocks_for(size_t n, int threads) { return (uint32_t)((n 
 // device and returns their address in *d_sums.
 // AF = coordinate field of the bucket pipeline (C::Fq, or FpR<Q> for the
 // reduced-radix form, whose bases are converted first).
+// prepared: d_bases already holds the pipeline's base records
+// (msm_prepare_t), so the per-call conversion is skipped.
 template <class C, class AF>
 int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
-                  const MsmPlan& pl, hipStream_t s, void** d_sums) {
+                  const MsmPlan& pl, hipStream_t s, void** d_sums, bool prepared) {
   using F = AF;
   using X = XYZZ<F>;
   const size_t m = (size_t)g.n_chunks * g.clen;  // scalars consumed
@@ -762,12 +764,14 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   const F* bases = (const F*)d_bases;
   if constexpr (!std::is_same<F, typename C::Fq>::value) {
     const size_t nb_in = (size_t)g.n_lines * g.line_len;  // every base a value can index
-    void* rb;
-    ECG_TRY(ws_get(ctx, "msm_rr_bases", nb_in * BaseLayout<F>::BYTES, &rb));
-    hipLaunchKernelGGL(msm_rr_bases_kernel<typename F::Params>, dim3(blocks_for(nb_in, MSM_THREADS)),
-                       dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, nb_in, (F*)rb);
-    ECG_HIP(hipGetLastError());
-    bases = (const F*)rb;
+    if (!prepared) {
+      void* rb;
+      ECG_TRY(ws_get(ctx, "msm_rr_bases", nb_in * BaseLayout<F>::BYTES, &rb));
+      hipLaunchKernelGGL(msm_rr_bases_kernel<typename F::Params>, dim3(blocks_for(nb_in, MSM_THREADS)),
+                         dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, nb_in, (F*)rb);
+      ECG_HIP(hipGetLastError());
+      bases = (const F*)rb;
+    }
   }
 
   hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(mpad, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
@@ -858,13 +862,47 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
 // Steps 1-6; leaves pl.G window sums (lazy 32-bit-limb XYZZ) on the device.
 template <class C>
 int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g, const MsmPlan& pl,
-               hipStream_t s, void** d_sums) {
+               hipStream_t s, void** d_sums, bool prepared = false) {
   if constexpr (has_rr_form<C>()) {
     if (msm_rr_enabled())
       return msm_core_impl<C, FpR<typename RRof<typename C::FqParams>::Q>>(ctx, d_bases, d_scalars, g, pl, s,
-                                                                            d_sums);
+                                                                            d_sums, prepared);
   }
-  return msm_core_impl<C, typename C::Fq>(ctx, d_bases, d_scalars, g, pl, s, d_sums);
+  return msm_core_impl<C, typename C::Fq>(ctx, d_bases, d_scalars, g, pl, s, d_sums, prepared);
+}
+
+// Bytes per base in the pipeline's own layout: 128-B reduced-radix records
+// (G1) or the [x, y] boundary layout (G2, or ECG_MSM_RR=0).
+template <class C>
+size_t msm_base_record_bytes() {
+  if constexpr (has_rr_form<C>()) {
+    if (msm_rr_enabled()) return BaseLayout<FpR<typename RRof<typename C::FqParams>::Q>>::BYTES;
+  }
+  return 2 * sizeof(typename C::Fq);
+}
+template <class C>
+size_t msm_prepared_bytes(size_t n) {
+  return n * msm_base_record_bytes<C>();
+}
+
+// upload_multiexp_bases (ag-cuda-ec/src/multiexp.rs:11-19): bases held on the
+// device in the layout the bucket kernels gather, converted once instead of
+// on every MSM over them (the conversion is ~2% of a 2^26 MSM).
+template <class C>
+int msm_prepare_t(ecg_ctx* ctx, const void* d_bases, size_t n, void* d_out, hipStream_t s) {
+  (void)ctx;
+  if (n == 0) return ECG_OK;
+  if constexpr (has_rr_form<C>()) {
+    if (msm_rr_enabled()) {
+      using AF = FpR<typename RRof<typename C::FqParams>::Q>;
+      hipLaunchKernelGGL(msm_rr_bases_kernel<typename AF::Params>, dim3(blocks_for(n, MSM_THREADS)),
+                         dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, n, (AF*)d_out);
+      ECG_HIP(hipGetLastError());
+      return ECG_OK;
+    }
+  }
+  ECG_HIP(hipMemcpyAsync(d_out, d_bases, n * 2 * sizeof(typename C::Fq), hipMemcpyDeviceToDevice, s));
+  return ECG_OK;
 }
 
 // Horner fold of one pass's W window sums (lazy device XYZZ) into `total`
@@ -922,7 +960,7 @@ size_t msm_pass_terms(const ecg_ctx* ctx) {
 // Horner fold of each pass and adds the passes up.
 template <class C>
 int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
-                        hipStream_t s, ecg_abort_cb abort_cb, void* user, uint32_t scalar_mont) {
+                        hipStream_t s, ecg_abort_cb abort_cb, void* user, uint32_t scalar_mont, bool prepared) {
   using F = typename C::Fq;
   using X = XYZZ<F>;
   using HX = host::HPoint<HostF<C>>;
@@ -936,7 +974,9 @@ int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_
     const MsmPlan pl = make_plan(m, (uint32_t)C::FrParams::BITS);
     const MsmGeom g{1, 1, m, m, scalar_mont};
     void* d_sums;
-    ECG_TRY(msm_core_t<C>(ctx, (const F*)d_bases + 2 * off, (const uint4*)d_scalars + 2 * off, g, pl, s, &d_sums));
+    const void* bp = prepared ? (const void*)((const char*)d_bases + off * msm_base_record_bytes<C>())
+                              : (const void*)((const F*)d_bases + 2 * off);
+    ECG_TRY(msm_core_t<C>(ctx, bp, (const uint4*)d_scalars + 2 * off, g, pl, s, &d_sums, prepared));
     // window sums -> host; Horner fold over windows (multiexp.rs:221-233)
     win.resize(pl.W);
     ECG_HIP(hipMemcpyAsync(win.data(), d_sums, pl.W * sizeof(X), hipMemcpyDeviceToHost, s));
@@ -1060,7 +1100,7 @@ int msm_host_t(ecg_ctx* ctx, const void* h_bases, const void* h_scalars, size_t 
 // line-major (results[line * n_chunks + chunk], multiexp.cl:260).
 template <class C>
 int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
-                       uint32_t window_bits, uint64_t* out_jac, hipStream_t s) {
+                       uint32_t window_bits, uint64_t* out_jac, hipStream_t s, bool prepared) {
   using F = typename C::Fq;
   kt_reset(ctx, "msm_accumulate");
   const uint32_t tasks = g.tasks();
@@ -1078,7 +1118,7 @@ int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const 
     return ECG_ERR_INVALID;
   }
   void *d_sums, *d_out;
-  ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums));
+  ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums, prepared));
   ECG_TRY(ws_get(ctx, "msm_batch_out", ob, &d_out));
   hipLaunchKernelGGL(msm_fold_kernel<C>, dim3(blocks_for(tasks, 64)), dim3(64), 0, s, (const XYZZ<F>*)d_sums, pl,
                      tasks, (F*)d_out);

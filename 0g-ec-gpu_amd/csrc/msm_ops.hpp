@@ -5,10 +5,15 @@
 namespace ecg {
 
 struct MsmOps {
+  // prepared: d_bases holds prepare()'s layout instead of [x, y]
   int (*single)(ecg_ctx*, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac, hipStream_t,
-                ecg_abort_cb, void* user, uint32_t scalar_mont);
+                ecg_abort_cb, void* user, uint32_t scalar_mont, bool prepared);
   int (*batch)(ecg_ctx*, const void* d_bases, const void* d_scalars, uint32_t n_lines, uint32_t n_chunks,
-               size_t line_len, uint32_t scalar_mont, uint32_t window_bits, uint64_t* out_jac, hipStream_t);
+               size_t line_len, uint32_t scalar_mont, uint32_t window_bits, uint64_t* out_jac, hipStream_t,
+               bool prepared);
+  // bases [x, y] -> the bucket kernels' layout (prepared_bytes(n) bytes at d_out)
+  int (*prepare)(ecg_ctx*, const void* d_bases, size_t n, void* d_out, hipStream_t);
+  size_t (*prepared_bytes)(size_t n);
   int (*point_sum)(const uint64_t* points, size_t count, uint64_t* out_jac);
   int (*gen_bases)(ecg_ctx*, const uint64_t* a, const uint64_t* b, size_t n, void* d_out, hipStream_t);
   size_t (*pass_terms)(const ecg_ctx*);

@@ -252,12 +252,18 @@ __global__ void __launch_bounds__(256)
 //   a1 = (s0 + 16r - s1) w2                     (<= 1.3 r)
 //   b0 = carry(d0 + d1)                         (<= 2.3 r)
 //   b1 = (d0 + 4r - d1) w2                      (<= 1.1 r)
-// The last step of a pass (h = 1: three of its four twiddles are 1) uses
-// reduce_q instead of those three products.
+// The last step of a pass (h = 1: three of its four twiddles are 1, or the
+// radix-2 round of an odd DEG) leaves its outputs unreduced ("P-form": limbs
+// < 2^31.4, value <= 21 r): they meet a product next -- the following pass
+// multiplies every element by its twiddle first, and a product of such an
+// operand with an exact twiddle is < r (1 + 21 * 2^-6.1) < 1.4 r with exact
+// limbs (column sums < 9 2^60.4 + 9 2^58 < 2^64) -- or rr_store_std's
+// reduce_q (limbs < 2^31.4, value < 64 r).  The first pass reads canonical
+// input and has no twiddle product, so P-form values never enter a sum.
 //
 // HBM layout: the transform's input and output are the boundary layout
 // (canonical, 8 packed words).  Between passes the elements stay in the
-// E-form as three planes (limbs 0-3 | 4-7 | 8: 36 B per element, coalesced
+// P-form as three planes (limbs 0-3 | 4-7 | 8: 36 B per element, coalesced
 // 16-B / 4-B accesses), so an inner pass boundary costs no unpacking,
 // reduction, canonicalisation or packing (~125 VALU instructions per element
 // saved for 4 more bytes).  The twiddle tables are planes of exact canonical
@@ -409,13 +415,16 @@ __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_pe
         rr_mul2(rr_sub_nc<16>(s0, s1), w2, rr_sub_nc<4>(d0, d1), w2, a1p, b1p);
         a1 = a1p;
         b1 = b1p;
-      } else {  // h = 1: qm = 0, so d1's twiddle w^(1 << r) is the only non-trivial one
+      } else {  // h = 1 (the pass's last step): qm = 0, only d1's twiddle w^(1 << r) is non-trivial
         const F d0 = rr_reduce_q(rr_sub_nc<8>(e0, e2));
         const F d1 = rr_mul(rr_sub_nc<8>(e1, e3), PQ.get((size_t)(1u << r) << pq_shift));
-        a0 = rr_reduce_q(rr_add_nc(s0, s1));
-        a1 = rr_reduce_q(rr_sub_nc<16>(s0, s1));
-        b0 = rr_carry_seq(rr_add_nc(d0, d1));
-        b1 = rr_reduce_q(rr_sub_nc<4>(d0, d1));
+        // Left unreduced ("P-form", see the header): every consumer -- the
+        // next pass's twiddle product or rr_store_std's reduce_q -- takes
+        // limbs < 2^31.4 and values < 64 r.
+        a0 = rr_add_nc(s0, s1);      // <= 10 r, limbs < 2^31
+        a1 = rr_sub_nc<16>(s0, s1);  // <= 21 r, limbs < 2^30 + 2^30.6
+        b0 = rr_add_nc(d0, d1);      // <= 2.3 r
+        b1 = rr_sub_nc<4>(d0, d1);   // <= 5.2 r, limbs < 2^29 + 2^30.6
       }
       U.put(pj, a0);
       U.put(pj ^ oh, a1);
@@ -424,12 +433,12 @@ __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_pe
     }
     __syncthreads();
   }
-  if (r < DEG) {  // odd DEG: last radix-2 round (bit = 1, trivial twiddles)
+  if (r < DEG) {  // odd DEG: last radix-2 round (bit = 1, trivial twiddles), outputs in the P-form
     for (uint32_t f = threadIdx.x; f < E / 2; f += blockDim.x) {
       const uint32_t p0 = lds_phys(2 * f);  // phys(2f + 1) = phys(2f) ^ 1
       const F u0 = U.get(p0), u1 = U.get(p0 ^ 1);
-      U.put(p0, rr_reduce_q(rr_add_nc(u0, u1)));
-      U.put(p0 ^ 1, rr_reduce_q(rr_sub_nc<8>(u0, u1)));
+      U.put(p0, rr_add_nc(u0, u1));           // <= 5 r
+      U.put(p0 ^ 1, rr_sub_nc<8>(u0, u1));    // <= 10.5 r, limbs < 2^29 + 2^30.6
     }
     __syncthreads();
   }
@@ -452,7 +461,7 @@ __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_pe
       const size_t dst = ((g - k) << DEG) + k + (uint64_t)jj * p;
       const F v = U.get(lds_phys((gi << DEG) + bitrev(jj, DEG)));
       if constexpr (OUT_RR)
-        RrPlanes<Q>::over(y, n).put(dst, v);  // E-form: the next pass multiplies it by its twiddle first
+        RrPlanes<Q>::over(y, n).put(dst, v);  // P-form: the next pass multiplies it by its twiddle first
       else
         rr_store_std<Q>(y, dst, v);
     }

@@ -85,6 +85,8 @@ _SIGS = {
                                      ctypes.c_size_t, _u64p, ABORT_CB, ctypes.c_void_p]),
     "ecg_msm_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                    ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "ecg_msm_prepare_bases": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_void_p)]),
     "ecg_point_sum_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, _u64p,
                                          ctypes.c_void_p]),
     "ecg_point_sum": (ctypes.c_int, [ctypes.c_int, _u64p, ctypes.c_size_t, _u64p]),
@@ -374,6 +376,35 @@ def msm_dev(prog: Program, curve, d_bases: DeviceBuffer, d_scalars: DeviceBuffer
     return out
 
 
+class PreparedBases(DeviceBuffer):
+    """Bases held in the bucket kernels' own layout (ecg_msm_prepare_bases):
+    the device-side half of upload_multiexp_bases (ag-cuda-ec/src/multiexp.rs:
+    11-19).  Pass it as d_bases / bases_gpu to msm_dev, multiple_multiexp or
+    dist.msm_dist; it is immutable and not readable as [x, y] records."""
+
+    def __init__(self, prog: Program, ptr: ctypes.c_void_p, curve_id: int, n: int):
+        self.program = prog
+        self.ptr = ptr
+        self.curve_id = curve_id
+        self.n = n
+        self.nbytes = 0
+
+    def write(self, host: np.ndarray) -> None:
+        raise EcError("PreparedBases are immutable: prepare new bases instead")
+
+    def read(self, dtype=np.uint64, shape=None) -> np.ndarray:
+        raise EcError("PreparedBases hold the kernels' internal layout")
+
+
+def prepare_bases(prog: Program, curve, d_bases: DeviceBuffer, n: int) -> PreparedBases:
+    """Convert n HBM-resident [x, y] bases once into the kernels' layout
+    (ecg_msm_prepare_bases); the MSMs over the result skip that conversion."""
+    cid = _curve(curve)
+    p = ctypes.c_void_p()
+    _check(lib().ecg_msm_prepare_bases(prog.handle, cid, d_bases.ptr, n, ctypes.byref(p)), "prepare_bases")
+    return PreparedBases(prog, p, cid, n)
+
+
 def fft_dev(prog: Program, field, d_data: DeviceBuffer, omega: np.ndarray, log_n: int) -> None:
     """In-place NTT of HBM-resident data (ecg_fft_dev)."""
     fid = _fft_field(field)
@@ -396,10 +427,17 @@ def gen_bases_dev(prog: Program, curve, a: int, b: int, n: int) -> DeviceBuffer:
 # ---------------------------------------------------------------------------
 
 
-def upload_multiexp_bases(prog: Program, bases: np.ndarray) -> DeviceBuffer:
+def upload_multiexp_bases(prog: Program, bases: np.ndarray, curve=None):
     """ag_cuda_ec::multiexp::upload_multiexp_bases (multiexp.rs:11-19): affine
-    bases (n, 2*Lq) u64, Montgomery x||y, identity = zeros (GpuRepr) -> HBM."""
-    return DeviceBuffer.upload(prog, np.ascontiguousarray(bases, dtype=np.uint64))
+    bases (n, 2*Lq) u64, Montgomery x||y, identity = zeros (GpuRepr) -> HBM.
+    With `curve` given, the upload is also converted once into the kernels'
+    layout (prepare_bases) and the PreparedBases are returned."""
+    raw = DeviceBuffer.upload(prog, np.ascontiguousarray(bases, dtype=np.uint64))
+    if curve is None:
+        return raw
+    prep = prepare_bases(prog, curve, raw, np.asarray(bases).shape[0])
+    raw.free()
+    return prep
 
 
 def multiple_multiexp(prog: Program, bases_gpu: DeviceBuffer, exponents, num_chunks: int,
@@ -428,7 +466,7 @@ def multiple_multiexp(prog: Program, bases_gpu: DeviceBuffer, exponents, num_chu
         sc_ptr, on_dev = keep.ctypes.data_as(ctypes.c_void_p), 0
     if line_len == 0:
         raise EcError("multiple_multiexp: empty exponent row")
-    n_bases = bases_gpu.nbytes // (2 * lq * 8)
+    n_bases = bases_gpu.n if isinstance(bases_gpu, PreparedBases) else bases_gpu.nbytes // (2 * lq * 8)
     n_lines = n_bases // line_len
     out = np.zeros((n_lines * num_chunks, 3 * lq), dtype=np.uint64)
     wb = int(window_size) if pin_window else 0

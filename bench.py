@@ -110,6 +110,8 @@ def parse(argv=None):
     ap.add_argument("--msm-cpu-log", type=int, default=24)
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive API timings (N=1)")
     ap.add_argument("--no-aux", action="store_true", help="skip the batched-MSM / EC-FFT side lines (N=1)")
+    ap.add_argument("--unprepared", action="store_true",
+                    help="time the MSM over [x, y] bases (conversion to the kernel layout inside every step)")
     return ap.parse_args(argv)
 
 
@@ -217,13 +219,19 @@ def main():
     i0, n_loc, scal, a_loc = msm_shard(rank, world, n_total, r_int)
     d_scal = ecgpu.DeviceBuffer.upload(prog, scal)
     d_bases = ecgpu.gen_bases_dev(prog, args.curve, a_loc, KAT_B, n_loc)
+    # upload_multiexp_bases (ag-cuda-ec/src/multiexp.rs:11-19): the resident
+    # bases are held in the bucket kernels' own layout (128-B reduced-radix
+    # records), converted once here -- as the reference uploads its bases once
+    # and reuses them across multiexps.  --unprepared keeps the [x, y] layout
+    # and converts inside every step.
+    d_msm_bases = d_bases if args.unprepared else ecgpu.prepare_bases(prog, args.curve, d_bases, n_loc)
     result = np.zeros(3 * lq, dtype=np.uint64)
 
-    def msm_step():
+    def msm_step(bases=d_msm_bases):
         if world == 1:
-            result[:] = ecgpu.msm_dev(prog, args.curve, d_bases, d_scal, n_loc)
+            result[:] = ecgpu.msm_dev(prog, args.curve, bases, d_scal, n_loc)
         else:  # local MSM + RCCL all-gather of world x 144 B partials + fold (no EC-add reduce op in RCCL)
-            result[:] = edist.msm_dist(prog, args.curve, d_bases, d_scal, n_loc)
+            result[:] = edist.msm_dist(prog, args.curve, bases, d_scal, n_loc)
 
     # ------------------------------------------------------------ NTT inputs (HBM-resident)
     log_n = args.ntt_log
@@ -259,6 +267,18 @@ def main():
     msm_s = group.max(time.perf_counter() - t0) / args.steps
     acc_avg_ms = group.max(acc_ms / max(acc_launch, 1))
     msm_result = result.copy()
+    # the same MSM over the [x, y] bases, converting them inside the step (reported, not `value`)
+    unprep_ms = None
+    if not args.unprepared:
+        msm_step(d_bases)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(2):
+            msm_step(d_bases)
+        barrier()
+        unprep_ms = group.max(time.perf_counter() - t0) / 2 * 1e3
+        if world == 1 and not (result == msm_result).all():
+            raise SystemExit("prepared and unprepared MSM results differ")
 
     # ------------------------------------------------------------ NTT timing (one transform per GPU)
     for _ in range(args.warmup):
@@ -441,10 +461,13 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "mod-p integer on v_mad_u64_u32 (MSM: 29-bit-limb reduced-radix Fq; NTT: u32-limb Fr)",
-        "data": "synthetic: bases (a+i*b)G generated on GPU, scalars uniform < r (seeded), HBM-resident",
+        "data": "synthetic: bases (a+i*b)G generated on GPU, scalars uniform < r (seeded), HBM-resident"
+                + ("" if args.unprepared else "; bases prepared once in the kernels' 128-B record layout "
+                   "(ecg_msm_prepare_bases, upload_multiexp_bases's role)"),
         "config": {"workload": f"{args.curve} G1 MSM 2^{args.msm_log} terms sharded over {world} GPU(s) "
                                f"+ Fr NTT 2^{log_n} per GPU", "msm_terms": n_total, "ntt_log_n": log_n,
                    "parallelism": f"range-shard x{world} + RCCL all-gather of partials" if world > 1 else "single GPU"},
+        "msm_ms_unprepared_bases": unprep_ms,
         "roofline": roofline,
         "ntt": {"metric": f"Fr NTT elements/sec @2^{log_n}", "value": world * n_ntt / ntt_s,
                 "unit": "elements/s", "ms_per_ntt": ntt_s * 1e3, "scaling": "weak (one transform per GPU)",

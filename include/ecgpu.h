@@ -159,6 +159,17 @@ int ecg_msm_multi(ecg_ctx **ctxs, int nctx, int curve_id, const uint64_t *bases_
 int ecg_msm_dev(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n,
                 void *out_jac, int out_on_device, void *stream);
 
+/* upload_multiexp_bases (ag-cuda-ec/src/multiexp.rs:11-19) in the engine's
+ * own layout: converts n device-resident [x, y] bases (d_bases, as
+ * ecg_msm_dev takes them) ONCE into a new device buffer in the layout the
+ * bucket kernels gather (G1: 128-B reduced-radix records; G2: [x, y]) and
+ * returns it in *d_prepared.  Pass *d_prepared as d_bases to ecg_msm_dev,
+ * ecg_multiple_multiexp or ecg_msm_dist (any call reading at most n bases of
+ * the same curve): those calls then skip the per-call conversion.  The
+ * buffer is immutable (re-prepare after changing the bases); release it
+ * with ecg_dev_free. */
+int ecg_msm_prepare_bases(ecg_ctx *ctx, int curve_id, const void *d_bases, size_t n, void **d_prepared);
+
 /* Batched multi-line MSM: ag_cuda_ec::multiexp::multiple_multiexp
  * (ag-cuda-ec/src/multiexp.rs:21-81; kernel ag-build/cl/multiexp.cl:215-262).
  * d_bases holds n_bases affine points (x, y Montgomery, identity = zeros) as

@@ -1,0 +1,141 @@
+"""GPU parity tests of prepared bases (ecg_msm_prepare_bases): the device-side
+half of ag-cuda-ec's upload_multiexp_bases (ag-cuda-ec/src/multiexp.rs:11-19)
+-- bases converted once into the bucket kernels' layout, then consumed by
+msm_dev, multiple_multiexp and the multi-pass MSM.  Checker: multiexp_cpu on
+the same bases (and the unprepared device path)."""
+import numpy as np
+import pytest
+
+import coracle as co
+import ecgpu
+import py_oracle as po
+
+pytestmark = pytest.mark.gpu
+
+CURVES = [("bls12_381", 0), ("bn254", 1), ("bls12_381_g2", 2), ("bn254_g2", 3)]
+
+
+def rand_scalars(cv, n, seed):
+    rng = po.Xoshiro256ss(seed)
+    return co.u64arr([rng.field_element(cv.fr) for _ in range(n)], 4)
+
+
+def same(cid, a, b):
+    x, y = co.jac_to_affine(cid, a), co.jac_to_affine(cid, b)
+    return (x is None and y is None) or (x is not None and y is not None and (x == y).all())
+
+
+@pytest.fixture(scope="module")
+def prog(gpu_programs):
+    return gpu_programs[0][0]
+
+
+@pytest.mark.parametrize("cname,cid", CURVES[:2])
+def test_prepared_msm_dev(prog, cname, cid):
+    """Prepared G1 bases (reduced-radix records) give the multiexp_cpu point,
+    for the whole array and for a shorter prefix; identity bases included."""
+    cv = po.CURVES[cname]
+    n = (1 << 16) + 77
+    d_b = ecgpu.gen_bases_dev(prog, cname, 31 + cid, 7, n)
+    B = d_b.read(shape=(n, -1))
+    B[5] = 0  # GpuRepr identity
+    d_b.write(B)
+    E = rand_scalars(cv, n, 40 + cid)
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    pb = ecgpu.prepare_bases(prog, cname, d_b, n)
+    want = co.multiexp_cpu(cid, np.delete(B, 5, axis=0), np.delete(E, 5, axis=0), nthreads=16)
+    assert same(cid, ecgpu.msm_dev(prog, cname, pb, d_e, n), want)
+    assert same(cid, ecgpu.msm_dev(prog, cname, d_b, d_e, n), want)
+    m = 1000  # a prefix of the prepared bases (the identity at 5 dropped for the CPU checker)
+    want_m = co.multiexp_cpu(cid, np.delete(B[:m], 5, axis=0), np.delete(E[:m], 5, axis=0), nthreads=8)
+    assert same(cid, ecgpu.msm_dev(prog, cname, pb, d_e, m), want_m)
+    pb.free()
+    d_b.free()
+    d_e.free()
+
+
+@pytest.mark.parametrize("cname,cid", CURVES[2:])
+def test_prepared_g2(prog, cname, cid):
+    """G2 keeps the [x, y] layout: prepared bases are a device copy and give
+    the same point as the unprepared path (itself pinned by test_gpu_g2)."""
+    n = (1 << 12) + 3
+    d_b = ecgpu.gen_bases_dev(prog, cname, 11 + cid, 13, n)
+    rng = np.random.default_rng(cid)
+    E = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+    E[:, 3] &= np.uint64(2**60 - 1)
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    want = ecgpu.msm_dev(prog, cname, d_b, d_e, n)
+    pb = ecgpu.prepare_bases(prog, cname, d_b, n)
+    d_b.free()
+    # both outputs are normalised Jacobian (x, y, 1) or (0, 1, 0): compare words
+    assert (ecgpu.msm_dev(prog, cname, pb, d_e, n) == want).all()
+    pb.free()
+    d_e.free()
+
+
+@pytest.mark.parametrize("cname,cid", CURVES[:2])
+def test_prepared_multi_pass(prog, cname, cid):
+    """Passes forced to 2^12 terms over prepared bases: per-pass record
+    offsets in the prepared layout."""
+    cv = po.CURVES[cname]
+    n = (1 << 14) + 37
+    B = co.gen_bases(cid, 900 + cid, 5, n, 8)
+    E = rand_scalars(cv, n, 910 + cid)
+    want = co.multiexp_cpu(cid, B, E, nthreads=16)
+    d_b = ecgpu.DeviceBuffer.upload(prog, B)
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    pb = ecgpu.prepare_bases(prog, cname, d_b, n)
+    prog.set_msm_chunk(1 << 12)
+    try:
+        assert same(cid, ecgpu.msm_dev(prog, cname, pb, d_e, n), want)
+    finally:
+        prog.set_msm_chunk(0)
+    pb.free()
+    d_b.free()
+    d_e.free()
+
+
+@pytest.mark.parametrize("cname,cid", CURVES[:2])
+def test_prepared_multiple_multiexp(prog, cname, cid):
+    """upload_multiexp_bases(curve=...) -> PreparedBases feed multiple_multiexp
+    (test_multiexp_batch shape: lines x chunks sharing one scalar row)."""
+    cv = po.CURVES[cname]
+    L, lines, chunks = 1 << 12, 3, 4
+    B = co.gen_bases(cid, 70 + cid, 3, L * lines, 8)
+    E = rand_scalars(cv, L, 80 + cid)
+    raw = ecgpu.upload_multiexp_bases(prog, B)
+    want = ecgpu.multiple_multiexp(prog, raw, E, chunks, curve=cname)
+    pb = ecgpu.upload_multiexp_bases(prog, B, curve=cname)
+    assert isinstance(pb, ecgpu.PreparedBases)
+    got = ecgpu.multiple_multiexp(prog, pb, E, chunks, curve=cname)
+    c = L // chunks
+    for t in range(lines * chunks):
+        line, ch = divmod(t, chunks)
+        assert same(cid, got[t], want[t])
+        if t in (0, lines * chunks - 1):
+            ref = co.multiexp_cpu(cid, B[line * L + ch * c:line * L + (ch + 1) * c], E[ch * c:(ch + 1) * c], nthreads=8)
+            assert same(cid, got[t], ref)
+    pb.free()
+    raw.free()
+
+
+def test_prepared_errors(prog):
+    """A prepared buffer serves only its curve and at most its n bases; freed
+    buffers are unregistered; PreparedBases cannot be written or read."""
+    n = 1 << 12
+    d_b = ecgpu.gen_bases_dev(prog, "bls12_381", 3, 5, n)
+    E = rand_scalars(po.CURVES["bls12_381"], n + 1, 7)
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    pb = ecgpu.prepare_bases(prog, "bls12_381", d_b, n)
+    with pytest.raises(ecgpu.EcError, match="prepared bases"):
+        ecgpu.msm_dev(prog, "bls12_381", pb, d_e, n + 1)
+    with pytest.raises(ecgpu.EcError, match="prepared bases"):
+        ecgpu.msm_dev(prog, "bn254", pb, d_e, 16)
+    with pytest.raises(ecgpu.EcError):
+        pb.write(E)
+    with pytest.raises(ecgpu.EcError):
+        pb.read()
+    pb.free()
+    pb.free()  # idempotent
+    d_b.free()
+    d_e.free()
