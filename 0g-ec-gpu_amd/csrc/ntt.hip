@@ -323,9 +323,10 @@ ECG_DEV void rr_store_std(uint4* __restrict__ y, size_t i, const FpR<Q>& v) {  /
 // (profiles/r02b/ntt_lds_swizzle.txt).
 ECG_HD constexpr uint32_t lds_phys(uint32_t j) { return j; }
 
-// 256-thread workgroups (tiles of <= 1024 elements): at the 1024-thread bound
-// (128 VGPRs) the products spilled
-constexpr uint32_t NTT_RR_THREADS = 512;
+// Up to 1024 threads (4096-element tiles, 147 KB of LDS: the 2-pass 2^24
+// schedule of ECG_NTT_MAXDEG=12); 4 waves/SIMD bound the kernel to 128 VGPRs
+// either way.
+constexpr uint32_t NTT_RR_THREADS = 1024;
 
 #ifndef ECG_NTT_RR_WAVES
 #define ECG_NTT_RR_WAVES 4
@@ -577,7 +578,7 @@ static hipError_t launch_pass_rr(const PassArgs& a, const RrTables& t, hipStream
   const size_t lds = (size_t)E * RR_PLANE_BYTES;
   uint32_t threads = E / NTT_EPT;
   if (threads < 64) threads = 64;
-  if (threads > NTT_RR_THREADS) return hipErrorInvalidValue;  // tiles of <= 2048 elements only
+  if (threads > NTT_RR_THREADS) return hipErrorInvalidValue;  // tiles of <= 4096 elements only
   auto kern = ntt_pass_rr_kernel<Q, DEG, IN_RR, OUT_RR>;
   static bool attr_set = false;  // > 64 KiB dynamic LDS needs an explicit opt-in
   if (!attr_set) {
@@ -612,6 +613,7 @@ static hipError_t launch_pass_rr_deg(int deg, bool in_rr, bool out_rr, const Pas
     case 9: return launch_pass_rr_io<Q, 9>(in_rr, out_rr, a, t, s);
     case 10: return launch_pass_rr_io<Q, 10>(in_rr, out_rr, a, t, s);
     case 11: return launch_pass_rr_io<Q, 11>(in_rr, out_rr, a, t, s);
+    case 12: return launch_pass_rr_io<Q, 12>(in_rr, out_rr, a, t, s);
     default: return hipErrorInvalidValue;
   }
 }
