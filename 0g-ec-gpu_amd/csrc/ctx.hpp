@@ -88,6 +88,7 @@ struct ecg_ctx {
   struct Prepared {
     int curve = -1;
     size_t n = 0;
+    uint32_t tab_c = 0;  // > 0: window table of window size tab_c (ecg_msm_prepare_table)
   };
   std::map<const void*, Prepared> prepared;
   // MSM terms per device pass (SingleMultiexpKernel::n, multiexp.rs:71-93);
@@ -150,7 +151,20 @@ void comm_free(ecg_ctx* ctx);
 int comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes, hipStream_t s);
 // Bases [x, y] -> a new device buffer in the bucket kernels' layout,
 // registered in ctx->prepared (ecg_msm_prepare_bases).
-int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, void** d_out, hipStream_t s);
+// How the bucket kernels read d_bases: the boundary [x, y] layout, prepared
+// records (ecg_msm_prepare_bases), or a window table (ecg_msm_prepare_table):
+// tab_c > 0, rows k = 0..W-1 of tab_n records 2^(k tab_c) P_i.
+struct BaseForm {
+  bool prepared = false;
+  uint32_t tab_c = 0;
+  size_t tab_n = 0;
+};
+
+// tab_c > 0: also the window table (rows 2^(k tab_c) P, ecg_msm_prepare_table).
+int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, uint32_t tab_c, void** d_out,
+                    hipStream_t s);
+// Window size of an automatic window table for n-term MSMs.
+uint32_t msm_table_window_auto(int curve_id, size_t n);
 int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const void* d_scalars,
                   int scalar_mont, size_t line_len, size_t n_chunks, uint32_t window_bits, uint64_t* out_jac,
                   hipStream_t s);

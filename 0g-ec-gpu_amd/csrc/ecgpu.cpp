@@ -438,7 +438,32 @@ int ecg_msm_prepare_bases(ecg_ctx* ctx, int curve_id, const void* d_bases, size_
     return ECG_ERR_INVALID;
   }
   *d_prepared = nullptr;
-  return msm_prepare_run(ctx, curve_id, d_bases, n, d_prepared, ctx->stream);
+  return msm_prepare_run(ctx, curve_id, d_bases, n, 0, d_prepared, ctx->stream);
+}
+
+uint32_t ecg_msm_table_window(int curve_id, size_t n) {
+  if (!curve_valid(curve_id)) return 0;
+  return msm_table_window_auto(curve_id, n);
+}
+
+int ecg_msm_prepare_table(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, uint32_t window_bits,
+                          void** d_prepared) {
+  ECG_ENTER(ctx);
+  if (!d_prepared || (!d_bases && n)) {
+    set_error("ecg_msm_prepare_table: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  if (!curve_valid(curve_id)) {
+    set_error("prepare_table: unknown curve_id %d", curve_id);
+    return ECG_ERR_INVALID;
+  }
+  if (n > 0x7fffffffull) {
+    set_error("prepare_table: at most 2^31-1 bases");
+    return ECG_ERR_INVALID;
+  }
+  *d_prepared = nullptr;
+  const uint32_t c = window_bits ? window_bits : msm_table_window_auto(curve_id, n);
+  return msm_prepare_run(ctx, curve_id, d_bases, n, c ? c : 2, d_prepared, ctx->stream);
 }
 
 int ecg_multiple_multiexp(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const uint64_t* scalars,

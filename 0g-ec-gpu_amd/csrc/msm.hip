@@ -22,11 +22,11 @@ static const MsmOps* msm_ops(int curve_id, const char* what) {
   }
 }
 
-// Is d_bases a prepared buffer (ecg_msm_prepare_bases)?  It must then cover
-// the n bases the call reads, for the same curve.
+// Is d_bases a prepared buffer (ecg_msm_prepare_bases / _table)?  It must
+// then cover the n bases the call reads, for the same curve.
 static int prepared_lookup(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, const char* what,
-                           bool* prepared) {
-  *prepared = false;
+                           BaseForm* bf) {
+  *bf = BaseForm{};
   auto it = ctx->prepared.find(d_bases);
   if (it == ctx->prepared.end()) return ECG_OK;
   if (it->second.curve != curve_id || n > it->second.n) {
@@ -34,7 +34,9 @@ static int prepared_lookup(ecg_ctx* ctx, int curve_id, const void* d_bases, size
               it->second.curve, n, curve_id);
     return ECG_ERR_INVALID;
   }
-  *prepared = true;
+  bf->prepared = true;
+  bf->tab_c = it->second.tab_c;
+  bf->tab_n = it->second.n;
   return ECG_OK;
 }
 
@@ -46,15 +48,36 @@ int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scala
   }
   const MsmOps* o = msm_ops(curve_id, "multiexp");
   if (!o) return ECG_ERR_INVALID;
-  bool prepared;
-  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n, "multiexp", &prepared));
-  return o->single(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0, prepared);
+  BaseForm bf;
+  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n, "multiexp", &bf));
+  return o->single(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0, bf);
 }
 
-int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, void** d_out, hipStream_t s) {
+uint32_t msm_table_window_auto(int curve_id, size_t n) {
+  const MsmOps* o = msm_ops(curve_id, "prepare_table");
+  return o ? o->table_auto(n) : 0;
+}
+
+int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, uint32_t tab_c, void** d_out,
+                    hipStream_t s) {
   const MsmOps* o = msm_ops(curve_id, "prepare_bases");
   if (!o) return ECG_ERR_INVALID;
-  const size_t bytes = o->prepared_bytes(n);
+  if (tab_c) {
+    if (tab_c < 2 || tab_c > 25) {
+      set_error("prepare_table: window size %u out of range [2, 25]", tab_c);
+      return ECG_ERR_INVALID;
+    }
+    const uint32_t W = o->table_windows(tab_c);
+    if (!W) {
+      set_error("prepare_table: window tables are built for the G1 curves only (curve %d)", curve_id);
+      return ECG_ERR_INVALID;
+    }
+    if ((uint64_t)W * n >= 0x80000000ull) {
+      set_error("prepare_table: %u rows x %zu bases exceeds the 2^31 table-index space", W, n);
+      return ECG_ERR_INVALID;
+    }
+  }
+  const size_t bytes = o->prepared_bytes(n, tab_c);
   void* p = nullptr;
   hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
   if (e != hipSuccess) {
@@ -62,7 +85,7 @@ int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, v
     set_error("prepare_bases: device allocation of %zu bytes failed: %s", bytes, hipGetErrorString(e));
     return ECG_ERR_NOMEM;
   }
-  int rc = o->prepare(ctx, d_bases, n, p, s);
+  int rc = o->prepare(ctx, d_bases, n, tab_c, p, s);
   if (rc == ECG_OK && hipStreamSynchronize(s) != hipSuccess) {
     set_error("prepare_bases: %s", hipGetErrorString(hipGetLastError()));
     rc = ECG_ERR_HIP;
@@ -71,7 +94,7 @@ int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, v
     (void)hipFree(p);
     return rc;
   }
-  ctx->prepared[p] = {curve_id, n};
+  ctx->prepared[p] = {curve_id, n, tab_c};
   *d_out = p;
   return ECG_OK;
 }
@@ -103,10 +126,10 @@ int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_base
   }
   const MsmOps* o = msm_ops(curve_id, "multiple_multiexp");
   if (!o) return ECG_ERR_INVALID;
-  bool prepared;
-  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n_bases, "multiple_multiexp", &prepared));
+  BaseForm bf;
+  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n_bases, "multiple_multiexp", &bf));
   return o->batch(ctx, d_bases, d_scalars, (uint32_t)n_lines, (uint32_t)n_chunks, line_len, scalar_mont != 0,
-                  window_bits, out_jac, s, prepared);
+                  window_bits, out_jac, s, bf);
 }
 
 int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac) {

@@ -58,17 +58,27 @@
 namespace ecg {
 
 constexpr int MSM_THREADS = 256;
-constexpr uint32_t MSM_FOLD = 32;        // fan-in of the partial-sum tree
+constexpr uint32_t MSM_TREE_K = 2;           // inputs per thread of the tree-sum kernel
 constexpr double MSM_MEMORY_PADDING = 0.2;    // share of HBM left free (multiexp.rs:24)
-constexpr uint32_t MSM_COMBINE_SEG = 32;      // records per thread in msm_combine
+constexpr uint32_t MSM_COMBINE_SEG_MAX = 32;  // records per thread in msm_combine (upper bound)
 
 // Tunables (env overrides for A/B measurement in one build).
 static uint32_t env_u32(const char* name, uint32_t dflt) {
   const char* e = getenv(name);
   return e ? (uint32_t)strtoul(e, nullptr, 10) : dflt;
 }
-static uint32_t msm_red_seg() {  // buckets per reduction segment
-  static uint32_t v = env_u32("ECG_MSM_RED_SEG", 64);
+static uint32_t msm_red_seg() {  // buckets per reduction segment (0: plan_reduction picks)
+  static uint32_t v = env_u32("ECG_MSM_RED_SEG", 0);
+  return v;
+}
+// Records per thread in msm_combine: each level is a serial chain of that many
+// adds, so the level count (log_seg of the records) matters less than the
+// depth: 8 measured 0.3 ms faster than 32 at 2^23 (profiles/r02d/ab_env.log).
+static uint32_t msm_combine_seg() {  // A/B: ECG_MSM_COMB_SEG
+  static uint32_t v = [] {
+    uint32_t x = env_u32("ECG_MSM_COMB_SEG", 8);
+    return x < 4 ? 4u : x > MSM_COMBINE_SEG_MAX ? MSM_COMBINE_SEG_MAX : x;
+  }();
   return v;
 }
 static uint32_t msm_acc_seg() {  // sorted entries per accumulation thread
@@ -107,7 +117,7 @@ static hipError_t msm_sort(int cfg, void* tmp, size_t& bytes, const uint64_t* ei
     default: return rocprim::radix_sort_keys(tmp, bytes, ei, eo, n, 32 + b0, 32 + b1, s);
   }
 }
-ECG_HD inline uint64_t msm_entry(uint32_t key, uint32_t val) { return ((uint64_t)key << 32) | val; }
+ECG_HD uint64_t msm_entry(uint32_t key, uint32_t val) { return ((uint64_t)key << 32) | val; }
 
 struct MsmPlan {
   uint32_t c;     // window bits
@@ -116,7 +126,9 @@ struct MsmPlan {
   uint32_t S;     // reduction segments per window
   uint32_t LS;    // buckets per segment
   uint32_t seg;   // sorted entries per accumulation thread
-  uint32_t G;     // bucket groups = tasks * W  (one group per (task, window))
+  uint32_t G;     // bucket groups = tasks * W  (one group per (task, window)); tasks with a window table
+  uint32_t tab;   // window-table mode: bases per table row (0 = off); every window shares its task's buckets
+  ECG_HD uint32_t fold_windows() const { return tab ? 1u : W; }  // window sums per task
 };
 
 // Task geometry.  A single MSM is one task (n_lines = n_chunks = 1).  The
@@ -135,6 +147,19 @@ struct MsmGeom {
   uint32_t tasks() const { return n_lines * n_chunks; }
 };
 
+// Buckets per reduction segment (LS; S = B / LS segments per group): the
+// running-sum chain of a segment is 2 LS dependent full adds, the offset
+// kernel then does one scalar multiple per segment.  64, or 32 when 64 would
+// leave fewer than 96K segments (< 1.5 waves per SIMD): 2^26 keeps 64 (106K),
+// the 2^23 shard of an 8-GPU run takes 32 (-0.4 ms; 16 was slower: 4x the
+// offset work, profiles/r02d/ab_env.log).  ECG_MSM_RED_SEG pins it (A/B).
+static void plan_reduction(MsmPlan& pl) {
+  uint32_t ls = msm_red_seg();
+  if (!ls) ls = (double)pl.G * pl.B / 64 < 96.0 * 1024 ? 32 : 64;
+  pl.LS = pl.B < ls ? pl.B : ls;
+  pl.S = pl.B / pl.LS;
+}
+
 // Window size minimising  n*W + W*B*4 + W*c*12  per task (bucket accumulation
 // vs reduction vs window-fold adds; a reduction step is ~2 full adds, ~1.4x a
 // mixed add).  nbits = scalar MODULUS_BIT_SIZE.  forced_c != 0 pins c.
@@ -152,10 +177,42 @@ static MsmPlan make_plan(size_t n, uint32_t nbits, uint32_t forced_c = 0) {
     }
   }
   pl.B = 1u << (pl.c - 1);
-  pl.LS = pl.B < msm_red_seg() ? pl.B : msm_red_seg();
-  pl.S = pl.B / pl.LS;
   pl.seg = msm_acc_seg();
   pl.G = pl.W;
+  pl.tab = 0;
+  plan_reduction(pl);
+  return pl;
+}
+
+// Window table (ecg_msm_prepare_table): row k of the table holds 2^(k c) P_i,
+// so the digit of window k of term i is a digit of base row k, and all W
+// windows of a task feed ONE set of 2^(c-1) buckets.  The W-fold bucket
+// reduction and the Horner fold disappear, which moves the best window from
+// c = 20 (13 windows at 2^26) to c = 24 (11 windows): 15% fewer mixed adds.
+// Cost model per term: W mixed adds; per bucket ~3 (2 full adds).
+static uint32_t table_window_auto(size_t n, uint32_t nbits) {
+  double best = 1e300;
+  uint32_t bc = 2;
+  for (uint32_t c = 2; c <= 25; c++) {
+    const uint32_t W = (nbits + 1 + c - 1) / c;
+    const double cost = (double)n * W + 3.0 * (double)(1u << (c - 1));
+    if (cost < best) {
+      best = cost;
+      bc = c;
+    }
+  }
+  return bc;
+}
+static uint32_t table_rows(uint32_t nbits, uint32_t c) { return (nbits + 1 + c - 1) / c; }
+static MsmPlan make_tab_plan(uint32_t tasks, uint32_t nbits, uint32_t c, size_t stride) {
+  MsmPlan pl{};
+  pl.c = c;
+  pl.W = table_rows(nbits, c);
+  pl.B = 1u << (c - 1);
+  pl.seg = msm_acc_seg();
+  pl.G = tasks;
+  pl.tab = (uint32_t)stride;
+  plan_reduction(pl);
   return pl;
 }
 
@@ -264,11 +321,13 @@ __global__ void __launch_bounds__(MSM_THREADS)
     const uint32_t mag = d < 0 ? (uint32_t)(-d) : (uint32_t)d;
     const uint32_t sign = d < 0 ? 0x80000000u : 0u;
     const size_t o = (size_t)w * mpad + j;
-    const uint32_t grp = chunk * pl.W + w;
+    // window table: every window of the task shares its buckets and reads base row w
+    const uint32_t grp = pl.tab ? chunk : chunk * pl.W + w;
+    const uint32_t bidx = pl.tab ? w * pl.tab + (uint32_t)j : (uint32_t)j;
     if (d == 0)
       ents[o] = msm_entry(km.kc ? (grp << km.kc) | km.B : km.sentinel, 0);
     else
-      ents[o] = msm_entry(km.kc ? (grp << km.kc) | (mag - 1) : grp * pl.B + (mag - 1), (uint32_t)j | sign);
+      ents[o] = msm_entry(km.kc ? (grp << km.kc) | (mag - 1) : grp * pl.B + (mag - 1), bidx | sign);
   }
 }
 
@@ -554,19 +613,51 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
 }
 
 // ---------------------------------------------------------------------------
-// 6. fold `cnt` consecutive points per group into ceil(cnt / MSM_FOLD)
+// 6. tree fold of `cnt` consecutive points per group: workgroup b of group g
+//    sums inputs [b * TREE_K * 256, (b+1) * TREE_K * 256): each thread adds
+//    TREE_K of them, then the workgroup halves its 256 points level by level in
+//    LDS -> one point per workgroup, out[g * wgs + b].  Depth TREE_K + 8 adds
+//    per launch (a fan-in-32 serial chain per thread was 32 per launch and
+//    latency-bound: 3 launches, 1.0 ms at 2^26).
 // ---------------------------------------------------------------------------
 template <class F>
-__global__ void __launch_bounds__(MSM_THREADS)
-    msm_sum_kernel(const XYZZ<F>* __restrict__ in, uint32_t W, uint32_t cnt, uint32_t out_cnt,
-                   XYZZ<F>* __restrict__ out) {
-  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= W * out_cnt) return;
-  const uint32_t w = id / out_cnt, o = id % out_cnt;
-  const uint32_t j0 = o * MSM_FOLD, j1 = min(j0 + MSM_FOLD, cnt);
+struct LdsPoints {  // XYZZ<F> words of point i at w[k * MSM_THREADS + i]
+  uint32_t* w;
+  static constexpr int NW = (int)(sizeof(XYZZ<F>) / 4);
+  ECG_DEV void put(uint32_t i, const XYZZ<F>& p) const {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(&p);
+#pragma unroll
+    for (int k = 0; k < NW; k++) w[k * MSM_THREADS + i] = s[k];
+  }
+  ECG_DEV XYZZ<F> get(uint32_t i) const {
+    XYZZ<F> p;
+    uint32_t* d = reinterpret_cast<uint32_t*>(&p);
+#pragma unroll
+    for (int k = 0; k < NW; k++) d[k] = w[k * MSM_THREADS + i];
+    return p;
+  }
+};
+
+template <class F>
+__global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
+    msm_tree_sum_kernel(const XYZZ<F>* __restrict__ in, uint32_t cnt, uint32_t wgs, XYZZ<F>* __restrict__ out) {
+  extern __shared__ uint32_t lds_pts[];
+  const LdsPoints<F> pts{lds_pts};
+  const uint32_t g = blockIdx.x / wgs, b = blockIdx.x % wgs, t = threadIdx.x;
+  const XYZZ<F>* src = in + (size_t)g * cnt;
+  const uint32_t j0 = (b * MSM_THREADS + t) * MSM_TREE_K;
   XYZZ<F> acc = xyzz_zero<F>();
-  for (uint32_t j = j0; j < j1; j++) acc = pa_add(acc, load_xyzz(&in[(size_t)w * cnt + j]));
-  store_xyzz(&out[id], acc);
+#pragma unroll 1
+  for (uint32_t k = 0; k < MSM_TREE_K; k++)
+    if (j0 + k < cnt) acc = pa_add(acc, load_xyzz(&src[j0 + k]));
+  pts.put(t, acc);
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t stride = MSM_THREADS / 2; stride > 0; stride >>= 1) {
+    if (t < stride) pts.put(t, pa_add(pts.get(t), pts.get(t + stride)));
+    __syncthreads();
+  }
+  if (t == 0) store_xyzz(&out[blockIdx.x], pts.get(0));
 }
 
 // ---------------------------------------------------------------------------
@@ -699,10 +790,11 @@ __global__ void __launch_bounds__(64)
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= tasks) return;
   XYZZ<F> acc = xyzz_zero<F>();
-  for (int w = (int)pl.W - 1; w >= 0; w--) {
-    if (w != (int)pl.W - 1)
+  const int nw = (int)pl.fold_windows();
+  for (int w = nw - 1; w >= 0; w--) {
+    if (w != nw - 1)
       for (uint32_t k = 0; k < pl.c; k++) acc = xyzz_dbl<F, true>(acc);
-    acc = xyzz_add<F, true>(acc, load_xyzz(&sums[(size_t)t * pl.W + w]));
+    acc = xyzz_add<F, true>(acc, load_xyzz(&sums[(size_t)t * nw + w]));
   }
   acc = xyzz_canon(acc);
   const bool id = xyzz_is_zero(acc);
@@ -733,7 +825,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   const uint32_t sentinel = nb;
   // window-padded keys (KeyMap) when every (window, line) block is one group
   // and large enough for a sort of its own
-  const bool pw = msm_pw_enabled() && g.n_chunks == 1 && m >= ((size_t)1 << 16) &&
+  const bool pw = msm_pw_enabled() && !pl.tab && g.n_chunks == 1 && m >= ((size_t)1 << 16) &&
                   ((uint64_t)(pl.G / g.n_lines) << pl.c) < 0xffffffffull;
   const size_t mpad = pw ? (m + pl.seg - 1) / pl.seg * pl.seg : m;
   // one line's entries (every line shares the scalar row; see msm_digits_kernel)
@@ -751,11 +843,13 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nb * sizeof(X), &bk));
   ECG_TRY(ws_get(ctx, "msm_recs", 2 * nseg_all * sizeof(X), &rc));
   ECG_TRY(ws_get(ctx, "msm_rkeys", 2 * nseg_all * 4, &rk));
-  const size_t nseg1 = (2 * nseg_all + MSM_COMBINE_SEG - 1) / MSM_COMBINE_SEG;
+  const uint32_t comb_seg = msm_combine_seg();
+  const size_t nseg1 = (2 * nseg_all + comb_seg - 1) / comb_seg;
   ECG_TRY(ws_get(ctx, "msm_recs2", 2 * nseg1 * sizeof(X), &rc2));
   ECG_TRY(ws_get(ctx, "msm_rkeys2", 2 * nseg1 * 4, &rk2));
   ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
-  ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * pl.S / MSM_FOLD + pl.G) * sizeof(X), &pb));
+  const uint32_t tree_span = MSM_TREE_K * MSM_THREADS;  // inputs per tree-sum workgroup
+  ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * ((pl.S + tree_span - 1) / tree_span) + pl.G) * sizeof(X), &pb));
 
   // buckets nobody writes (no term) stay the identity: all-zero XYZZ (ZZ = 0).
   // (Running this clear and the base conversion on a side stream, concurrent
@@ -810,10 +904,10 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   X* rout = (X*)rc2;
   uint32_t* kout = (uint32_t*)rk2;
   for (;;) {
-    const bool fin = nrec <= MSM_COMBINE_SEG;
-    const size_t nthr = (nrec + MSM_COMBINE_SEG - 1) / MSM_COMBINE_SEG;
+    const bool fin = nrec <= comb_seg;
+    const size_t nthr = (nrec + comb_seg - 1) / comb_seg;
     hipLaunchKernelGGL(msm_combine_kernel<F>, dim3(blocks_for(nthr, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                       (const X*)rin, (const uint32_t*)kin, nrec, sentinel, MSM_COMBINE_SEG, fin ? 1 : 0, (X*)bk,
+                       (const X*)rin, (const uint32_t*)kin, nrec, sentinel, comb_seg, fin ? 1 : 0, (X*)bk,
                        rout, kout);
     ECG_HIP(hipGetLastError());
     if (fin) break;
@@ -834,15 +928,19 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   uint32_t cnt = pl.S;
   X* in = (X*)pa;
   X* out = (X*)pb;
+  const size_t tree_lds = (size_t)LdsPoints<F>::NW * MSM_THREADS * 4;
+  if (tree_lds > 64 * 1024)  // G2 points (96 KiB per workgroup) need the opt-in
+    ECG_HIP(hipFuncSetAttribute((const void*)msm_tree_sum_kernel<F>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)tree_lds));
   while (cnt > 1) {
-    const uint32_t oc = (cnt + MSM_FOLD - 1) / MSM_FOLD;
-    hipLaunchKernelGGL(msm_sum_kernel<F>, dim3(blocks_for((size_t)pl.G * oc, MSM_THREADS)), dim3(MSM_THREADS),
-                       0, s, (const X*)in, pl.G, cnt, oc, out);
+    const uint32_t wgs = (cnt + tree_span - 1) / tree_span;
+    hipLaunchKernelGGL(msm_tree_sum_kernel<F>, dim3(pl.G * wgs), dim3(MSM_THREADS), tree_lds, s, (const X*)in, cnt,
+                       wgs, out);
     ECG_HIP(hipGetLastError());
     X* t = in;
     in = out;
     out = t;
-    cnt = oc;
+    cnt = wgs;
   }
   if constexpr (std::is_same<F, typename C::Fq>::value) {
     *d_sums = in;
@@ -879,17 +977,86 @@ size_t msm_base_record_bytes() {
   return 2 * sizeof(typename C::Fq);
 }
 template <class C>
-size_t msm_prepared_bytes(size_t n) {
-  return n * msm_base_record_bytes<C>();
+uint32_t msm_table_windows(uint32_t tab_c) {  // rows of a window table (G1 only)
+  return C::EXT == 1 && tab_c >= 2 ? table_rows((uint32_t)C::FrParams::BITS, tab_c) : 0u;
+}
+template <class C>
+uint32_t msm_table_auto(size_t n) {
+  return C::EXT == 1 ? table_window_auto(n, (uint32_t)C::FrParams::BITS) : 0u;
+}
+template <class C>
+size_t msm_prepared_bytes(size_t n, uint32_t tab_c) {
+  return n * msm_base_record_bytes<C>() * (tab_c ? msm_table_windows<C>(tab_c) : 1u);
+}
+
+// Window-table rows (ecg_msm_prepare_table): row k+1 = 2^c row k.
+// 1. c doublings per base (in the pipeline's point form AF), out as strict
+//    32-bit-limb XYZZ;
+// 2. batch normalisation to affine: one Fermat inversion per TAB_NORM_BLOCK
+//    points (Montgomery's trick, as gen_bases_kernel);
+// 3. the pipeline's record conversion (msm_rr_bases_kernel) into the row.
+constexpr uint32_t TAB_NORM_BLOCK = 32;
+template <class C, class AF>
+__global__ void __launch_bounds__(MSM_THREADS)
+    msm_tab_dbl_kernel(const typename C::Fq* __restrict__ in, size_t n, uint32_t c,
+                       XYZZ<typename C::Fq>* __restrict__ out) {
+  using F = typename C::Fq;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Affine<F> a = load_affine(in + 2 * i);
+  if (aff_is_identity(a)) {  // GpuRepr identity: every multiple is the identity
+    store_xyzz(&out[i], xyzz_zero<F>());
+    return;
+  }
+  if constexpr (std::is_same<AF, F>::value) {
+    XYZZ<F> p = xyzz_dbl_affine(a);
+    for (uint32_t k = 1; k < c; k++) p = xyzz_dbl(p);
+    store_xyzz(&out[i], p);
+  } else {
+    XYZZ<AF> p = pa_from_std_rr<typename AF::Params>(xyzz_from_affine(a));
+    for (uint32_t k = 0; k < c; k++) p = pa_dbl(p);
+    store_xyzz(&out[i], xyzz_canon(pa_to_std(p)));
+  }
+}
+
+template <class C>
+__global__ void __launch_bounds__(MSM_THREADS)
+    msm_tab_norm_kernel(const XYZZ<typename C::Fq>* __restrict__ pts, size_t n, typename C::Fq* __restrict__ pref,
+                        typename C::Fq* __restrict__ out) {
+  using F = typename C::Fq;
+  const size_t i0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * TAB_NORM_BLOCK;
+  if (i0 >= n) return;
+  const uint32_t cnt = (uint32_t)min((size_t)TAB_NORM_BLOCK, n - i0);
+  F acc = F::one();
+  for (uint32_t k = 0; k < cnt; k++) {
+    const XYZZ<F> p = load_xyzz(&pts[i0 + k]);
+    store(&pref[i0 + k], acc);
+    if (!xyzz_is_zero(p)) acc = fmul(acc, fmul(p.ZZ, p.ZZZ));
+  }
+  F inv = finv(acc);
+  for (int k = (int)cnt - 1; k >= 0; k--) {
+    const size_t i = i0 + k;
+    const XYZZ<F> p = load_xyzz(&pts[i]);
+    Affine<F> r;
+    if (xyzz_is_zero(p)) {
+      r.x = F::zero();
+      r.y = F::zero();
+    } else {
+      const F d_inv = fmul(inv, load(&pref[i]));  // 1 / (ZZ ZZZ) of point i
+      inv = fmul(inv, fmul(p.ZZ, p.ZZZ));
+      r.x = fmul(p.X, fmul(d_inv, p.ZZZ));
+      r.y = fmul(p.Y, fmul(d_inv, p.ZZ));
+    }
+    store(&out[2 * i], r.x);
+    store(&out[2 * i + 1], r.y);
+  }
 }
 
 // upload_multiexp_bases (ag-cuda-ec/src/multiexp.rs:11-19): bases held on the
 // device in the layout the bucket kernels gather, converted once instead of
 // on every MSM over them (the conversion is ~2% of a 2^26 MSM).
 template <class C>
-int msm_prepare_t(ecg_ctx* ctx, const void* d_bases, size_t n, void* d_out, hipStream_t s) {
-  (void)ctx;
-  if (n == 0) return ECG_OK;
+int msm_records_t(const void* d_bases, size_t n, void* d_out, hipStream_t s) {  // [x, y] -> records
   if constexpr (has_rr_form<C>()) {
     if (msm_rr_enabled()) {
       using AF = FpR<typename RRof<typename C::FqParams>::Q>;
@@ -903,13 +1070,71 @@ int msm_prepare_t(ecg_ctx* ctx, const void* d_bases, size_t n, void* d_out, hipS
   return ECG_OK;
 }
 
+template <class C, class AF>
+int msm_table_rows_t(const void* d_bases, size_t n, uint32_t tab_c, void* d_out, hipStream_t s) {
+  using F = typename C::Fq;
+  const uint32_t W = msm_table_windows<C>(tab_c);
+  const size_t rec = msm_base_record_bytes<C>();
+  const size_t sl = std::min(n, (size_t)1 << 22);  // bases per slice (bounded scratch)
+  void *pts = nullptr, *pref = nullptr, *aff[2] = {nullptr, nullptr};
+  int rc = ECG_OK;
+  auto fail = [&](hipError_t e) {
+    (void)hipGetLastError();
+    set_error("prepare_table: %s", hipGetErrorString(e));
+    rc = e == hipErrorOutOfMemory ? ECG_ERR_NOMEM : ECG_ERR_HIP;
+  };
+  hipError_t e = hipMalloc(&pts, sl * sizeof(XYZZ<F>));
+  if (e == hipSuccess) e = hipMalloc(&pref, sl * sizeof(F));
+  if (e == hipSuccess) e = hipMalloc(&aff[0], sl * 2 * sizeof(F));
+  if (e == hipSuccess) e = hipMalloc(&aff[1], sl * 2 * sizeof(F));
+  if (e != hipSuccess) fail(e);
+  for (size_t a = 0; rc == ECG_OK && a < n; a += sl) {
+    const size_t len = std::min(sl, n - a);
+    const F* cur = (const F*)d_bases + 2 * a;
+    for (uint32_t k = 1; rc == ECG_OK && k < W; k++) {
+      F* nxt = (F*)aff[k & 1];
+      hipLaunchKernelGGL((msm_tab_dbl_kernel<C, AF>), dim3(blocks_for(len, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                         cur, len, tab_c, (XYZZ<F>*)pts);
+      hipLaunchKernelGGL(msm_tab_norm_kernel<C>, dim3(blocks_for((len + TAB_NORM_BLOCK - 1) / TAB_NORM_BLOCK, 64)),
+                         dim3(64), 0, s, (const XYZZ<F>*)pts, len, (F*)pref, nxt);
+      if ((e = hipGetLastError()) != hipSuccess) {
+        fail(e);
+        break;
+      }
+      rc = msm_records_t<C>(nxt, len, (char*)d_out + ((size_t)k * n + a) * rec, s);
+      cur = nxt;
+    }
+  }
+  if (rc == ECG_OK && (e = hipStreamSynchronize(s)) != hipSuccess) fail(e);
+  for (void* p : {pts, pref, aff[0], aff[1]})
+    if (p) (void)hipFree(p);
+  return rc;
+}
+
+template <class C>
+int msm_prepare_t(ecg_ctx* ctx, const void* d_bases, size_t n, uint32_t tab_c, void* d_out, hipStream_t s) {
+  (void)ctx;
+  if (n == 0) return ECG_OK;
+  ECG_TRY(msm_records_t<C>(d_bases, n, d_out, s));  // table row 0 = the bases themselves
+  if (!tab_c) return ECG_OK;
+  if constexpr (C::EXT == 1) {
+    if constexpr (has_rr_form<C>()) {
+      if (msm_rr_enabled())
+        return msm_table_rows_t<C, FpR<typename RRof<typename C::FqParams>::Q>>(d_bases, n, tab_c, d_out, s);
+    }
+    return msm_table_rows_t<C, typename C::Fq>(d_bases, n, tab_c, d_out, s);
+  }
+  set_error("prepare_table: window tables are built for the G1 curves only");
+  return ECG_ERR_INVALID;
+}
+
 // Horner fold of one pass's W window sums (lazy device XYZZ) into `total`
 // on the host (multiexp.rs:221-233).
 template <class C>
 void msm_host_fold(const XYZZ<typename C::Fq>* win, const MsmPlan& pl, host::HPoint<HostF<C>>& total) {
   using HX = host::HPoint<HostF<C>>;
   HX acc = HX::zero();
-  for (int w = (int)pl.W - 1; w >= 0; w--) {
+  for (int w = (int)pl.fold_windows() - 1; w >= 0; w--) {
     for (uint32_t k = 0; k < pl.c; k++) acc = host::hdbl(acc);
     HX ww;
     static_assert(sizeof(ww.X) == sizeof(win[w].X), "host/device coordinate layouts differ");
@@ -958,7 +1183,8 @@ size_t msm_pass_terms(const ecg_ctx* ctx) {
 // Horner fold of each pass and adds the passes up.
 template <class C>
 int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
-                        hipStream_t s, ecg_abort_cb abort_cb, void* user, uint32_t scalar_mont, bool prepared) {
+                        hipStream_t s, ecg_abort_cb abort_cb, void* user, uint32_t scalar_mont, BaseForm bf) {
+  const bool prepared = bf.prepared;
   using F = typename C::Fq;
   using X = XYZZ<F>;
   using HX = host::HPoint<HostF<C>>;
@@ -969,15 +1195,16 @@ int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_
   for (size_t off = 0; off < n; off += chunk) {
     if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144
     const size_t m = n - off < chunk ? n - off : chunk;
-    const MsmPlan pl = make_plan(m, (uint32_t)C::FrParams::BITS);
+    const MsmPlan pl = bf.tab_c ? make_tab_plan(1, (uint32_t)C::FrParams::BITS, bf.tab_c, bf.tab_n)
+                                : make_plan(m, (uint32_t)C::FrParams::BITS);
     const MsmGeom g{1, 1, m, m, scalar_mont};
     void* d_sums;
     const void* bp = prepared ? (const void*)((const char*)d_bases + off * msm_base_record_bytes<C>())
                               : (const void*)((const F*)d_bases + 2 * off);
     ECG_TRY(msm_core_t<C>(ctx, bp, (const uint4*)d_scalars + 2 * off, g, pl, s, &d_sums, prepared));
     // window sums -> host; Horner fold over windows (multiexp.rs:221-233)
-    win.resize(pl.W);
-    ECG_HIP(hipMemcpyAsync(win.data(), d_sums, pl.W * sizeof(X), hipMemcpyDeviceToHost, s));
+    win.resize(pl.fold_windows());
+    ECG_HIP(hipMemcpyAsync(win.data(), d_sums, win.size() * sizeof(X), hipMemcpyDeviceToHost, s));
     ECG_HIP(hipStreamSynchronize(s));
     msm_host_fold<C>(win.data(), pl, total_acc);
   }
@@ -1098,8 +1325,9 @@ int msm_host_t(ecg_ctx* ctx, const void* h_bases, const void* h_scalars, size_t 
 // line-major (results[line * n_chunks + chunk], multiexp.cl:260).
 template <class C>
 int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
-                       uint32_t window_bits, uint64_t* out_jac, hipStream_t s, bool prepared) {
+                       uint32_t window_bits, uint64_t* out_jac, hipStream_t s, BaseForm bf) {
   using F = typename C::Fq;
+  const bool prepared = bf.prepared;
   kt_reset(ctx, "msm_accumulate");
   const uint32_t tasks = g.tasks();
   const size_t ob = (size_t)tasks * 3 * sizeof(F);
@@ -1108,8 +1336,14 @@ int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const 
     for (uint32_t t = 0; t < tasks; t++) host::hto_jac_norm(HX::zero(), out_jac + (size_t)t * 3 * HostF<C>::N);
     return ECG_OK;
   }
-  MsmPlan pl = make_plan(g.clen, (uint32_t)C::FrParams::BITS, window_bits);
-  pl.G = tasks * pl.W;
+  MsmPlan pl;
+  if (bf.tab_c) {  // the table fixes the window (window_size is a tuning hint, results never depend on it)
+    pl = make_tab_plan(tasks, (uint32_t)C::FrParams::BITS, bf.tab_c, bf.tab_n);
+  } else {
+    pl = make_plan(g.clen, (uint32_t)C::FrParams::BITS, window_bits);
+    pl.G = tasks * pl.W;
+    plan_reduction(pl);
+  }
   if ((uint64_t)pl.G * pl.B >= 0xffffffffull) {
     set_error("multiple_multiexp: %u tasks x %u windows x %u buckets exceeds the 32-bit bucket space", tasks, pl.W,
               pl.B);

@@ -5,15 +5,17 @@
 namespace ecg {
 
 struct MsmOps {
-  // prepared: d_bases holds prepare()'s layout instead of [x, y]
   int (*single)(ecg_ctx*, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac, hipStream_t,
-                ecg_abort_cb, void* user, uint32_t scalar_mont, bool prepared);
+                ecg_abort_cb, void* user, uint32_t scalar_mont, BaseForm bf);
   int (*batch)(ecg_ctx*, const void* d_bases, const void* d_scalars, uint32_t n_lines, uint32_t n_chunks,
                size_t line_len, uint32_t scalar_mont, uint32_t window_bits, uint64_t* out_jac, hipStream_t,
-               bool prepared);
-  // bases [x, y] -> the bucket kernels' layout (prepared_bytes(n) bytes at d_out)
-  int (*prepare)(ecg_ctx*, const void* d_bases, size_t n, void* d_out, hipStream_t);
-  size_t (*prepared_bytes)(size_t n);
+               BaseForm bf);
+  // bases [x, y] -> the bucket kernels' layout (prepared_bytes(n, tab_c) bytes at d_out); tab_c > 0 builds
+  // the window table (G1 only)
+  int (*prepare)(ecg_ctx*, const void* d_bases, size_t n, uint32_t tab_c, void* d_out, hipStream_t);
+  size_t (*prepared_bytes)(size_t n, uint32_t tab_c);
+  uint32_t (*table_windows)(uint32_t tab_c);  // rows of a window table (0: no table form for this curve)
+  uint32_t (*table_auto)(size_t n);           // window size of an automatic table for n-term MSMs
   int (*point_sum)(const uint64_t* points, size_t count, uint64_t* out_jac);
   int (*gen_bases)(ecg_ctx*, const uint64_t* a, const uint64_t* b, size_t n, void* d_out, hipStream_t);
   size_t (*pass_terms)(const ecg_ctx*);

@@ -87,6 +87,8 @@ _SIGS = {
                                    ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "ecg_msm_prepare_bases": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                              ctypes.POINTER(ctypes.c_void_p)]),
+    "ecg_msm_prepare_table": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
     "ecg_point_sum_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, _u64p,
                                          ctypes.c_void_p]),
     "ecg_point_sum": (ctypes.c_int, [ctypes.c_int, _u64p, ctypes.c_size_t, _u64p]),
@@ -108,6 +110,7 @@ _SIGS = {
     "ecg_msm_chunk_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "ecg_ctx_set_msm_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
     "ecg_runtime_info": (ctypes.c_char_p, []),
+    "ecg_msm_table_window": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_size_t]),
     "ecg_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "ecg_comm_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]),
     "ecg_comm_destroy": (None, [ctypes.c_void_p]),
@@ -384,11 +387,12 @@ class PreparedBases(DeviceBuffer):
     11-19).  Pass it as d_bases / bases_gpu to msm_dev, multiple_multiexp or
     dist.msm_dist; it is immutable and not readable as [x, y] records."""
 
-    def __init__(self, prog: Program, ptr: ctypes.c_void_p, curve_id: int, n: int):
+    def __init__(self, prog: Program, ptr: ctypes.c_void_p, curve_id: int, n: int, window_table: int = 0):
         self.program = prog
         self.ptr = ptr
         self.curve_id = curve_id
         self.n = n
+        self.window_table = window_table  # 0, or the window size of the precomputed table
         self.nbytes = 0
 
     def write(self, host: np.ndarray) -> None:
@@ -398,13 +402,20 @@ class PreparedBases(DeviceBuffer):
         raise EcError("PreparedBases hold the kernels' internal layout")
 
 
-def prepare_bases(prog: Program, curve, d_bases: DeviceBuffer, n: int) -> PreparedBases:
+def prepare_bases(prog: Program, curve, d_bases: DeviceBuffer, n: int, window_table=None) -> PreparedBases:
     """Convert n HBM-resident [x, y] bases once into the kernels' layout
-    (ecg_msm_prepare_bases); the MSMs over the result skip that conversion."""
+    (ecg_msm_prepare_bases); the MSMs over the result skip that conversion.
+    window_table: None = plain records; 0 = precompute the window table for
+    n-term MSMs (window chosen by the engine); c = table of window size c
+    (ecg_msm_prepare_table, G1 only)."""
     cid = _curve(curve)
     p = ctypes.c_void_p()
-    _check(lib().ecg_msm_prepare_bases(prog.handle, cid, d_bases.ptr, n, ctypes.byref(p)), "prepare_bases")
-    return PreparedBases(prog, p, cid, n)
+    if window_table is None:
+        _check(lib().ecg_msm_prepare_bases(prog.handle, cid, d_bases.ptr, n, ctypes.byref(p)), "prepare_bases")
+        return PreparedBases(prog, p, cid, n)
+    _check(lib().ecg_msm_prepare_table(prog.handle, cid, d_bases.ptr, n, int(window_table), ctypes.byref(p)),
+           "prepare_table")
+    return PreparedBases(prog, p, cid, n, window_table=int(window_table) or -1)
 
 
 def fft_dev(prog: Program, field, d_data: DeviceBuffer, omega: np.ndarray, log_n: int) -> None:
@@ -429,15 +440,16 @@ def gen_bases_dev(prog: Program, curve, a: int, b: int, n: int) -> DeviceBuffer:
 # ---------------------------------------------------------------------------
 
 
-def upload_multiexp_bases(prog: Program, bases: np.ndarray, curve=None):
+def upload_multiexp_bases(prog: Program, bases: np.ndarray, curve=None, window_table=None):
     """ag_cuda_ec::multiexp::upload_multiexp_bases (multiexp.rs:11-19): affine
     bases (n, 2*Lq) u64, Montgomery x||y, identity = zeros (GpuRepr) -> HBM.
     With `curve` given, the upload is also converted once into the kernels'
-    layout (prepare_bases) and the PreparedBases are returned."""
+    layout (prepare_bases, optionally with a window table) and the
+    PreparedBases are returned."""
     raw = DeviceBuffer.upload(prog, np.ascontiguousarray(bases, dtype=np.uint64))
     if curve is None:
         return raw
-    prep = prepare_bases(prog, curve, raw, np.asarray(bases).shape[0])
+    prep = prepare_bases(prog, curve, raw, np.asarray(bases).shape[0], window_table=window_table)
     raw.free()
     return prep
 

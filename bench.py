@@ -110,6 +110,8 @@ def parse(argv=None):
     ap.add_argument("--msm-cpu-log", type=int, default=24)
     ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive API timings (N=1)")
     ap.add_argument("--no-aux", action="store_true", help="skip the batched-MSM / EC-FFT side lines (N=1)")
+    ap.add_argument("--no-table", action="store_true",
+                    help="skip the window-table (fixed-base) MSM leg (ecg_msm_prepare_table)")
     ap.add_argument("--unprepared", action="store_true",
                     help="time the MSM over [x, y] bases (conversion to the kernel layout inside every step)")
     return ap.parse_args(argv)
@@ -280,6 +282,29 @@ def main():
         if not (result == msm_result).all():  # every rank holds the folded result
             raise SystemExit("prepared and unprepared MSM results differ")
 
+    # the same MSM over a window table of the bases (fixed-base form, ecg_msm_prepare_table): reported
+    # beside `value`, which stays on the per-call base layout the reference's API takes
+    table = None
+    if not args.no_table and not args.unprepared and cid in (0, 1):
+        msm_prep = d_msm_bases
+        t0 = time.perf_counter()
+        d_tab = ecgpu.prepare_bases(prog, args.curve, d_bases, n_loc, window_table=0)
+        prep_s = group.max(time.perf_counter() - t0)
+        msm_step(d_tab)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            msm_step(d_tab)
+        barrier()
+        tab_s = group.max(time.perf_counter() - t0) / args.steps
+        table = {"ms": tab_s * 1e3, "value": n_total / tab_s, "unit": "point-adds/s",
+                 "window": ecgpu.lib().ecg_msm_table_window(cid, n_loc), "prepare_s": prep_s,
+                 "equals_headline_result": bool((result == msm_result).all()),
+                 "note": "bases prepared with their 2^(k c) multiples (W rows): every window feeds one bucket set; "
+                         "same inputs and result as `value`, table built once outside the timed region"}
+        d_tab.free()
+        del msm_prep
+
     # ------------------------------------------------------------ NTT timing (one transform per GPU)
     for _ in range(args.warmup):
         ntt_step()
@@ -404,6 +429,21 @@ def main():
         mm_s = time.perf_counter() - t_a
         aux["multiple_multiexp"] = {"shape": f"{lines} lines x 2^21, {chunks} chunks/line ({L // chunks} terms/task)",
                                     "ms": mm_s * 1e3, "terms_per_s": L * lines / mm_s}
+        if not args.no_table and cid in (0, 1):
+            # the AMT bases are uploaded once and reused (upload_multiexp_bases): window table for 2^11-term tasks
+            mm_ref = ecgpu.multiple_multiexp(prog, d_lb, (d_le, L), chunks, curve=args.curve)
+            tw = ecgpu.lib().ecg_msm_table_window(cid, L // chunks)
+            t_a = time.perf_counter()
+            d_lt = ecgpu.prepare_bases(prog, args.curve, d_lb, L * lines, window_table=tw)
+            lt_prep = time.perf_counter() - t_a
+            ecgpu.multiple_multiexp(prog, d_lt, (d_le, L), chunks, curve=args.curve)
+            t_a = time.perf_counter()
+            mm_t = ecgpu.multiple_multiexp(prog, d_lt, (d_le, L), chunks, curve=args.curve)
+            mt_s = time.perf_counter() - t_a
+            aux["multiple_multiexp_window_table"] = {"window": tw, "prepare_s": lt_prep, "ms": mt_s * 1e3,
+                                                     "terms_per_s": L * lines / mt_s,
+                                                     "equal": bool((mm_t == mm_ref).all())}
+            d_lt.free()
         d_lb.free()
         d_le.free()
         # G1 EC-FFT 2^16 (tests/ec_fft.rs top size)
@@ -488,6 +528,7 @@ def main():
                                f"+ Fr NTT 2^{log_n} per GPU", "msm_terms": n_total, "ntt_log_n": log_n,
                    "parallelism": f"range-shard x{world} + RCCL all-gather of partials" if world > 1 else "single GPU"},
         "msm_ms_unprepared_bases": unprep_ms,
+        "msm_window_table": table,
         "roofline": roofline,
         "ntt": {"metric": f"Fr NTT elements/sec @2^{log_n}", "value": world * n_ntt / ntt_s,
                 "unit": "elements/s", "ms_per_ntt": ntt_s * 1e3, "scaling": "weak (one transform per GPU)",

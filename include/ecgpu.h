@@ -170,6 +170,23 @@ int ecg_msm_dev(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_s
  * with ecg_dev_free. */
 int ecg_msm_prepare_bases(ecg_ctx *ctx, int curve_id, const void *d_bases, size_t n, void **d_prepared);
 
+/* Fixed-base form of ecg_msm_prepare_bases for bases reused across many
+ * MSMs (upload_multiexp_bases's use in ag-cuda-ec, multiexp.rs:11-19): also
+ * precomputes the window table 2^(k c) P_i for the W = ceil(256 / c) windows
+ * (c = window_bits; 0 = chosen for an n-term MSM: 24 at 2^26).  MSMs over
+ * the returned buffer put every window's digit into ONE bucket set, which
+ * removes the per-window bucket reduction and admits a larger window (fewer
+ * mixed adds per term).  Same results as any other base form.  Memory: W x
+ * the prepared records (2^26 BLS12-381 bases at c = 24: 11 x 8 GiB).
+ * G1 curves only; W x n < 2^31.  Use and release as ecg_msm_prepare_bases. */
+int ecg_msm_prepare_table(ecg_ctx *ctx, int curve_id, const void *d_bases, size_t n, uint32_t window_bits,
+                          void **d_prepared);
+
+/* The window size ecg_msm_prepare_table picks (window_bits = 0) for MSMs of
+ * n terms -- for multiple_multiexp pass the chunk length.  0 for curves
+ * without a table form (G2) or an unknown curve_id. */
+uint32_t ecg_msm_table_window(int curve_id, size_t n);
+
 /* Batched multi-line MSM: ag_cuda_ec::multiexp::multiple_multiexp
  * (ag-cuda-ec/src/multiexp.rs:21-81; kernel ag-build/cl/multiexp.cl:215-262).
  * d_bases holds n_bases affine points (x, y Montgomery, identity = zeros) as
