@@ -147,17 +147,28 @@ struct MsmGeom {
   uint32_t tasks() const { return n_lines * n_chunks; }
 };
 
-// Buckets per reduction segment (LS; S = B / LS segments per group): the
-// running-sum chain of a segment is 2 LS dependent full adds, the offset
-// kernel then does one scalar multiple per segment.  64, or 32 when 64 would
-// leave fewer than 96K segments (< 1.5 waves per SIMD): 2^26 keeps 64 (106K),
-// the 2^23 shard of an 8-GPU run takes 32 (-0.4 ms; 16 was slower: 4x the
-// offset work, profiles/r02d/ab_env.log).  ECG_MSM_RED_SEG pins it (A/B).
+// Buckets per reduction segment (LS; S = ceil(B / LS) segments per group,
+// the last one possibly shorter).  A segment's running sums are a chain of
+// 2 LS dependent full adds and the kernel is VALU-bound at 2 waves per SIMD,
+// so what matters is that every SIMD gets the same share: with LS = 64 a
+// 2^26 MSM has 13 x 8192 segments = 1.63 waves per SIMD, i.e. half the SIMDs
+// run two 128-step chains while the others idle for the second.  Below
+// MSM_RED_THREADS segments (2 waves on each of the 1024 SIMDs) the groups'
+// buckets are therefore cut into exactly that many equal segments (any
+// length: the offset kernel multiplies by the segment's first index).
+// ECG_MSM_RED_SEG pins LS (A/B).
+constexpr uint32_t MSM_RED_THREADS = 2 * 1024 * 64;
 static void plan_reduction(MsmPlan& pl) {
   uint32_t ls = msm_red_seg();
-  if (!ls) ls = (double)pl.G * pl.B / 64 < 96.0 * 1024 ? 32 : 64;
+  if (!ls) {
+    ls = 64;
+    if ((double)pl.G * pl.B / 64 < MSM_RED_THREADS) {
+      const uint32_t per_group = std::max(1u, MSM_RED_THREADS / pl.G);
+      ls = (pl.B + per_group - 1) / per_group;
+    }
+  }
   pl.LS = pl.B < ls ? pl.B : ls;
-  pl.S = pl.B / pl.LS;
+  pl.S = (pl.B + pl.LS - 1) / pl.LS;
 }
 
 // Window size minimising  n*W + W*B*4 + W*c*12  per task (bucket accumulation
@@ -580,9 +591,10 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
   if (id >= pl.G * pl.S) return;
   const uint32_t w = id / pl.S, sgm = id % pl.S;
   const XYZZ<F>* bk = buckets + (size_t)w * pl.B + (size_t)sgm * pl.LS;
+  const uint32_t len = min(pl.LS, pl.B - sgm * pl.LS);  // the last segment may be shorter
   XYZZ<F> run = xyzz_zero<F>();
   acc_l.put(xyzz_zero<F>());
-  for (int j = (int)pl.LS - 1; j >= 0; j--) {
+  for (int j = (int)len - 1; j >= 0; j--) {
     run = pa_add(run, load_xyzz(&bk[j]));
     acc_l.put(pa_add(acc_l.get(), run));
   }
