@@ -153,7 +153,7 @@ int comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes,
 // registered in ctx->prepared (ecg_msm_prepare_bases).
 // How the bucket kernels read d_bases: the boundary [x, y] layout, prepared
 // records (ecg_msm_prepare_bases), or a window table (ecg_msm_prepare_table):
-// tab_c > 0, rows k = 0..W-1 of tab_n records 2^(k tab_c) P_i.
+// tab_c > 0, record i W + k = 2^(k tab_c) P_i for the tab_n bases, k < W.
 struct BaseForm {
   bool prepared = false;
   uint32_t tab_c = 0;

@@ -127,7 +127,7 @@ struct MsmPlan {
   uint32_t LS;    // buckets per segment
   uint32_t seg;   // sorted entries per accumulation thread
   uint32_t G;     // bucket groups = tasks * W  (one group per (task, window)); tasks with a window table
-  uint32_t tab;   // window-table mode: bases per table row (0 = off); every window shares its task's buckets
+  uint32_t tab;   // window-table mode: bases in the table (0 = off); every window shares its task's buckets
   ECG_HD uint32_t fold_windows() const { return tab ? 1u : W; }  // window sums per task
 };
 
@@ -195,18 +195,23 @@ static MsmPlan make_plan(size_t n, uint32_t nbits, uint32_t forced_c = 0) {
   return pl;
 }
 
-// Window table (ecg_msm_prepare_table): row k of the table holds 2^(k c) P_i,
+// Window table (ecg_msm_prepare_table): row k of the table holds 2^(k c) P_i
+// (record i W + k: the W rows of a base are adjacent, so a task's gathers stay
+// inside its own bases' records -- rows of their own, 2.7 GB apart on the AMT
+// shape, made every gather a TLB miss: 2.7x slower accumulation),
 // so the digit of window k of term i is a digit of base row k, and all W
 // windows of a task feed ONE set of 2^(c-1) buckets.  The W-fold bucket
 // reduction and the Horner fold disappear, which moves the best window from
 // c = 20 (13 windows at 2^26) to c = 24 (11 windows): 15% fewer mixed adds.
-// Cost model per term: W mixed adds; per bucket ~3 (2 full adds).
+// Cost model per term: W mixed adds; per bucket ~5 (2 full adds + the combine
+// and reduction launches: the AMT shape measures c = 11 fastest, 75.4 vs
+// 77.6 ms at c = 12).
 static uint32_t table_window_auto(size_t n, uint32_t nbits) {
   double best = 1e300;
   uint32_t bc = 2;
   for (uint32_t c = 2; c <= 25; c++) {
     const uint32_t W = (nbits + 1 + c - 1) / c;
-    const double cost = (double)n * W + 3.0 * (double)(1u << (c - 1));
+    const double cost = (double)n * W + 5.0 * (double)(1u << (c - 1));
     if (cost < best) {
       best = cost;
       bc = c;
@@ -332,9 +337,10 @@ __global__ void __launch_bounds__(MSM_THREADS)
     const uint32_t mag = d < 0 ? (uint32_t)(-d) : (uint32_t)d;
     const uint32_t sign = d < 0 ? 0x80000000u : 0u;
     const size_t o = (size_t)w * mpad + j;
-    // window table: every window of the task shares its buckets and reads base row w
+    // window table: every window of the task shares its buckets and reads row w
+    // of base j, record j * W + w (the rows of a base sit together)
     const uint32_t grp = pl.tab ? chunk : chunk * pl.W + w;
-    const uint32_t bidx = pl.tab ? w * pl.tab + (uint32_t)j : (uint32_t)j;
+    const uint32_t bidx = pl.tab ? (uint32_t)j * pl.W + w : (uint32_t)j;
     if (d == 0)
       ents[o] = msm_entry(km.kc ? (grp << km.kc) | km.B : km.sentinel, 0);
     else
@@ -672,13 +678,31 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
   if (t == 0) store_xyzz(&out[blockIdx.x], pts.get(0));
 }
 
+// A few points per group (batched MSMs: 2 reduction segments per (task,
+// window)): one thread per group adds them serially.  A tree-sum workgroup per
+// group would run 8 LDS levels of adds for 2 inputs (13.9 ms on the AMT shape,
+// 327680 workgroups).
+constexpr uint32_t MSM_GROUP_SERIAL = 16;
+template <class F>
+__global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
+    msm_group_sum_kernel(const XYZZ<F>* __restrict__ in, uint32_t cnt, uint32_t groups, XYZZ<F>* __restrict__ out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= groups) return;
+  const XYZZ<F>* src = in + (size_t)g * cnt;
+  XYZZ<F> acc = load_xyzz(&src[0]);
+#pragma unroll 1
+  for (uint32_t k = 1; k < cnt; k++) acc = pa_add(acc, load_xyzz(&src[k]));
+  store_xyzz(&out[g], acc);
+}
+
 // ---------------------------------------------------------------------------
 // reduced-radix pipeline (curve_rr.hpp): bases into the R' form before step 3,
 // window sums back to the 32-bit-limb form after step 6
 // ---------------------------------------------------------------------------
 template <class Q>
 __global__ void __launch_bounds__(MSM_THREADS)
-    msm_rr_bases_kernel(const Fp<typename Q::Base>* __restrict__ in, size_t n, FpR<Q>* __restrict__ out) {
+    msm_rr_bases_kernel(const Fp<typename Q::Base>* __restrict__ in, size_t n, uint32_t stride,
+                        FpR<Q>* __restrict__ out) {
   using F = Fp<typename Q::Base>;
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -691,7 +715,7 @@ __global__ void __launch_bounds__(MSM_THREADS)
     r.x = rr_from_std<Q>(a.x);
     r.y = rr_from_std<Q>(a.y);
   }
-  FpR<Q>* rec = base_ptr(out, i);
+  FpR<Q>* rec = base_ptr(out, i * stride);  // stride > 1: one row of an interleaved window table
   store_affine(rec, r);
   // zero the record's pad too: whole-line writes (a partial line costs a
   // read-modify-write; measured 3.3 -> 5.6 ms for this kernel without it)
@@ -874,7 +898,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
       void* rb;
       ECG_TRY(ws_get(ctx, "msm_rr_bases", nb_in * BaseLayout<F>::BYTES, &rb));
       hipLaunchKernelGGL(msm_rr_bases_kernel<typename F::Params>, dim3(blocks_for(nb_in, MSM_THREADS)),
-                         dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, nb_in, (F*)rb);
+                         dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, nb_in, 1u, (F*)rb);
       ECG_HIP(hipGetLastError());
       bases = (const F*)rb;
     }
@@ -902,7 +926,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   // (13 launch tails, and the concurrent sort slows the VALU-bound
   // accumulation by as much as it hides)
   ECG_TRY(kt_begin(ctx, "msm_accumulate", s));
-  const AccLines ln{g.n_lines, g.line_len, line_groups * pl.B};
+  const AccLines ln{g.n_lines, pl.tab ? g.line_len * pl.W : g.line_len, line_groups * pl.B};
   hipLaunchKernelGGL(msm_accumulate_kernel<F>, dim3(blocks_for(nseg_all, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
                      bases, (const uint64_t*)e1, total, km, pl.seg, nseg, ln, (X*)bk, (X*)rc,
                      (uint32_t*)rk);
@@ -944,6 +968,13 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   if (tree_lds > 64 * 1024)  // G2 points (96 KiB per workgroup) need the opt-in
     ECG_HIP(hipFuncSetAttribute((const void*)msm_tree_sum_kernel<F>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)tree_lds));
+  if (cnt > 1 && cnt <= MSM_GROUP_SERIAL) {
+    hipLaunchKernelGGL(msm_group_sum_kernel<F>, dim3(blocks_for(pl.G, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                       (const X*)in, cnt, pl.G, out);
+    ECG_HIP(hipGetLastError());
+    std::swap(in, out);
+    cnt = 1;
+  }
   while (cnt > 1) {
     const uint32_t wgs = (cnt + tree_span - 1) / tree_span;
     hipLaunchKernelGGL(msm_tree_sum_kernel<F>, dim3(pl.G * wgs), dim3(MSM_THREADS), tree_lds, s, (const X*)in, cnt,
@@ -1067,18 +1098,24 @@ __global__ void __launch_bounds__(MSM_THREADS)
 // upload_multiexp_bases (ag-cuda-ec/src/multiexp.rs:11-19): bases held on the
 // device in the layout the bucket kernels gather, converted once instead of
 // on every MSM over them (the conversion is ~2% of a 2^26 MSM).
+// [x, y] -> records; record i goes to slot i * stride of d_out (stride = W:
+// one row of an interleaved window table).
 template <class C>
-int msm_records_t(const void* d_bases, size_t n, void* d_out, hipStream_t s) {  // [x, y] -> records
+int msm_records_t(const void* d_bases, size_t n, void* d_out, hipStream_t s, uint32_t stride = 1) {
   if constexpr (has_rr_form<C>()) {
     if (msm_rr_enabled()) {
       using AF = FpR<typename RRof<typename C::FqParams>::Q>;
       hipLaunchKernelGGL(msm_rr_bases_kernel<typename AF::Params>, dim3(blocks_for(n, MSM_THREADS)),
-                         dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, n, (AF*)d_out);
+                         dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, n, stride, (AF*)d_out);
       ECG_HIP(hipGetLastError());
       return ECG_OK;
     }
   }
-  ECG_HIP(hipMemcpyAsync(d_out, d_bases, n * 2 * sizeof(typename C::Fq), hipMemcpyDeviceToDevice, s));
+  const size_t rb = 2 * sizeof(typename C::Fq);
+  if (stride == 1)
+    ECG_HIP(hipMemcpyAsync(d_out, d_bases, n * rb, hipMemcpyDeviceToDevice, s));
+  else if (n)
+    ECG_HIP(hipMemcpy2DAsync(d_out, stride * rb, d_bases, rb, rb, n, hipMemcpyDeviceToDevice, s));
   return ECG_OK;
 }
 
@@ -1113,7 +1150,7 @@ int msm_table_rows_t(const void* d_bases, size_t n, uint32_t tab_c, void* d_out,
         fail(e);
         break;
       }
-      rc = msm_records_t<C>(nxt, len, (char*)d_out + ((size_t)k * n + a) * rec, s);
+      rc = msm_records_t<C>(nxt, len, (char*)d_out + ((size_t)a * W + k) * rec, s, W);
       cur = nxt;
     }
   }
@@ -1127,7 +1164,8 @@ template <class C>
 int msm_prepare_t(ecg_ctx* ctx, const void* d_bases, size_t n, uint32_t tab_c, void* d_out, hipStream_t s) {
   (void)ctx;
   if (n == 0) return ECG_OK;
-  ECG_TRY(msm_records_t<C>(d_bases, n, d_out, s));  // table row 0 = the bases themselves
+  // table row 0 = the bases themselves
+  ECG_TRY(msm_records_t<C>(d_bases, n, d_out, s, tab_c ? msm_table_windows<C>(tab_c) : 1u));
   if (!tab_c) return ECG_OK;
   if constexpr (C::EXT == 1) {
     if constexpr (has_rr_form<C>()) {
@@ -1211,7 +1249,8 @@ int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_
                                 : make_plan(m, (uint32_t)C::FrParams::BITS);
     const MsmGeom g{1, 1, m, m, scalar_mont};
     void* d_sums;
-    const void* bp = prepared ? (const void*)((const char*)d_bases + off * msm_base_record_bytes<C>())
+    const void* bp = prepared ? (const void*)((const char*)d_bases + off * msm_base_record_bytes<C>() *
+                                              (bf.tab_c ? pl.W : 1u))
                               : (const void*)((const F*)d_bases + 2 * off);
     ECG_TRY(msm_core_t<C>(ctx, bp, (const uint4*)d_scalars + 2 * off, g, pl, s, &d_sums, prepared));
     // window sums -> host; Horner fold over windows (multiexp.rs:221-233)
