@@ -1,4 +1,5 @@
-"""Run the 2^N MSM a few times (profiling target, dev tool)."""
+"""Run the 2^N MSM a few times (profiling target, dev tool).
+Usage: python tools/msm_once.py [log_n] [reps] [prepared: 0|1]"""
 import os, sys, numpy as np
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "0g-ec-gpu_amd"))
 import ecgpu
@@ -10,6 +11,8 @@ rng = np.random.default_rng(7)
 E = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64); E[:, 3] &= np.uint64(2**62 - 1)
 d_e = ecgpu.DeviceBuffer.upload(prog, E)
 d_b = ecgpu.gen_bases_dev(prog, "bls12_381", 12345, 678910, n)
+if len(sys.argv) > 3 and sys.argv[3] == "1":
+    d_b = ecgpu.prepare_bases(prog, "bls12_381", d_b, n)
 for _ in range(reps):
     ecgpu.msm_dev(prog, "bls12_381", d_b, d_e, n)
 print("done")

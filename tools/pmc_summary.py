@@ -1,4 +1,4 @@
-"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/gpu_prof.sh)
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/gpu.sh prof)
 into profiles/<tag>/pmc_fetch_write.json (mean KB per dispatch per kernel) and
 copy the kernel-trace stats next to it.  Usage: python tools/pmc_summary.py <tag>"""
 import csv
