@@ -1,0 +1,352 @@
+// G2 in the reduced-radix form: Fq2 = Fq[u]/(u^2 + 1) over the 29-/28-bit-limb
+// Montgomery elements of fieldrr.hpp, and the XYZZ formulas of curve_rr.hpp
+// restated over it (madd-2008-s, add-2008-s, dbl-2008-s-1 / mdbl-2008-s-1;
+// ec.cl:17-130 and field2.cl:1-61's roles for the MSM bucket pipeline).
+//
+// An Fq2 product is two one-reduction product sums (rr_mul_sum2):
+//   c0 = (a0 b0 + a1 (K p - b1)) / R',  c1 = (a0 b1 + a1 b0) / R'
+// -- 4 products and 2 reductions, the same mad count as Karatsuba's 3 + 3 with
+// no operand sums; a square is the complex method as one interleaved pair,
+//   c0 = (a0 + a1)(a0 - a1 + K p) / R',  c1 = (2 a0) a1 / R'.
+// Every output component is a product output (exact limbs, value < p (1 + 2^-9)),
+// so the zero screens of curve_rr.hpp work per component.
+//
+// Bounds (units of p, per component; M = product output):
+//   stored points  X <= 17.01, Y <= 4.01, ZZ, ZZZ <= M;  bases x <= M,
+//                  y <= M or 4p - y (carried: every G2 product operand is QN)
+//   madd:  P = U2 - X1 + 64p <= 65, R = S2 - Y1 + 16p <= 17,
+//          X3 = R^2 - PPP - 2Q + 16p <= 17.01, D = Q - X3 + 64p <= 65,
+//          Y3 = D R + Y1 (4p - PPP)   (two product outputs summed) <= 2.01
+//   add:   P, R <= 5.01, the rest as madd;  dbl: U = 2Y <= 8.02, M = 3X^2 <= 3.01
+// The K of each negated operand is at least twice its bound; the largest
+// product sum is 130 x 321 p^2 (the square of P), far inside the 2^24 p^2 that
+// the 2^25 slack of rr_mul allows.
+#pragma once
+#include "curve_rr.hpp"
+#include "field2.hpp"
+
+namespace ecg {
+
+template <class Q>
+struct FpR2 {
+  using Params = Q;
+  using Base = FpR<Q>;
+  FpR<Q> c0, c1;
+  ECG_DEV static FpR2 zero() {
+    FpR2 r;
+    r.c0 = FpR<Q>::zero();
+    r.c1 = FpR<Q>::zero();
+    return r;
+  }
+  ECG_DEV static FpR2 one() {
+    FpR2 r;
+    r.c0 = FpR<Q>::one();
+    r.c1 = FpR<Q>::zero();
+    return r;
+  }
+};
+
+template <class Q>
+ECG_DEV FpR2<Q> mkr2(const FpR<Q>& a, const FpR<Q>& b) {
+  FpR2<Q> r;
+  r.c0 = a;
+  r.c1 = b;
+  return r;
+}
+
+// a b; b.c1 <= K p / 2
+template <int K, class Q>
+ECG_DEV FpR2<Q> r2_mul(const FpR2<Q>& a, const FpR2<Q>& b) {
+  return mkr2(rr_mul_sum2(a.c0, b.c0, a.c1, rr_neg<K>(b.c1)), rr_mul_sum2(a.c0, b.c1, a.c1, b.c0));
+}
+// a^2; a.c1 <= K p / 2
+template <int K, class Q>
+ECG_DEV FpR2<Q> r2_sqr(const FpR2<Q>& a) {
+  FpR2<Q> r;
+  rr_mul2(rr_add(a.c0, a.c1), rr_sub<K>(a.c0, a.c1), rr_add(a.c0, a.c0), a.c1, r.c0, r.c1);
+  return r;
+}
+template <class Q>
+ECG_DEV FpR2<Q> r2_add(const FpR2<Q>& a, const FpR2<Q>& b) {
+  return mkr2(rr_add(a.c0, b.c0), rr_add(a.c1, b.c1));
+}
+template <int K, class Q>
+ECG_DEV FpR2<Q> r2_sub(const FpR2<Q>& a, const FpR2<Q>& b) {
+  return mkr2(rr_sub<K>(a.c0, b.c0), rr_sub<K>(a.c1, b.c1));
+}
+template <int K, class Q>
+ECG_DEV FpR2<Q> r2_sub2(const FpR2<Q>& a, const FpR2<Q>& b, const FpR2<Q>& c) {
+  return mkr2(rr_sub2<K>(a.c0, b.c0, c.c0), rr_sub2<K>(a.c1, b.c1, c.c1));
+}
+template <int K, class Q>
+ECG_DEV FpR2<Q> r2_sub3(const FpR2<Q>& a, const FpR2<Q>& b, const FpR2<Q>& c, const FpR2<Q>& d) {
+  return mkr2(rr_sub3<K>(a.c0, b.c0, c.c0, d.c0), rr_sub3<K>(a.c1, b.c1, c.c1, d.c1));
+}
+template <int K, class Q>
+ECG_DEV FpR2<Q> r2_neg(const FpR2<Q>& a) {
+  return mkr2(rr_neg<K>(a.c0), rr_neg<K>(a.c1));
+}
+template <class Q>
+ECG_DEV bool fis_zero(const FpR2<Q>& a) {
+  return fis_zero(a.c0) && fis_zero(a.c1);
+}
+template <class Q>
+ECG_DEV bool r2_is_zero_prod(const FpR2<Q>& a) {
+  return rr_is_zero_prod(a.c0) && rr_is_zero_prod(a.c1);
+}
+template <class Q>
+ECG_DEV bool r2_maybe_zero_prod(const FpR2<Q>& a) {
+  return rr_maybe_zero_prod(a.c0) && rr_maybe_zero_prod(a.c1);
+}
+template <class Q>
+ECG_DEV void rr_sel(FpR2<Q>& r, bool c, const FpR2<Q>& s) {
+  rr_sel(r.c0, c, s.c0);
+  rr_sel(r.c1, c, s.c1);
+}
+template <class Q>
+ECG_DEV void rr_sel(XYZZ<FpR2<Q>>& r, bool c, const XYZZ<FpR2<Q>>& s) {
+  rr_sel(r.X, c, s.X);
+  rr_sel(r.Y, c, s.Y);
+  rr_sel(r.ZZ, c, s.ZZ);
+  rr_sel(r.ZZZ, c, s.ZZZ);
+}
+
+// ark-ff Fq2 (c0, c1 Montgomery, < p) <-> the reduced-radix form
+template <class Q>
+ECG_DEV FpR2<Q> rr2_from_std(const Fp2<typename Q::Base>& a) {
+  return mkr2(rr_from_std<Q>(a.c0), rr_from_std<Q>(a.c1));
+}
+template <class Q>
+ECG_DEV Fp2<typename Q::Base> rr2_to_std(const FpR2<Q>& a) {
+  return mk2(rr_to_std(a.c0), rr_to_std(a.c1));
+}
+
+// ---------------------------------------------------------------------------
+// XYZZ formulas (the bounds in the header)
+// ---------------------------------------------------------------------------
+// dbl-2008-s-1 core on (X, Y): new X, Y and the ZZ, ZZZ factors V = U^2, W = U V
+template <class Q>
+ECG_DEV void r2_dbl_core(const FpR2<Q>& X, const FpR2<Q>& Y, XYZZ<FpR2<Q>>& r, FpR2<Q>& V, FpR2<Q>& W) {
+  const FpR2<Q> U = r2_add(Y, Y);
+  V = r2_sqr<64>(U);
+  const FpR2<Q> X2 = r2_sqr<64>(X);
+  W = r2_mul<4>(U, V);
+  const FpR2<Q> S = r2_mul<4>(X, V);
+  const FpR2<Q> Mm = r2_add(r2_add(X2, X2), X2);
+  r.X = r2_sub2<16>(r2_sqr<8>(Mm), S, S);
+  r.Y = r2_add(r2_mul<8>(r2_sub<64>(S, r.X), Mm), r2_mul<8>(Y, r2_neg<4>(W)));
+}
+
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> r2_dbl_affine(const Affine<FpR2<Q>>& a) {
+  XYZZ<FpR2<Q>> r;
+  r2_dbl_core(a.x, a.y, r, r.ZZ, r.ZZZ);
+  return r;
+}
+
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> r2_dbl(const XYZZ<FpR2<Q>>& p) {
+  if (fis_zero(p.ZZ)) return p;
+  XYZZ<FpR2<Q>> r;
+  FpR2<Q> V, W;
+  r2_dbl_core(p.X, p.Y, r, V, W);
+  r.ZZ = r2_mul<4>(p.ZZ, V);
+  r.ZZZ = r2_mul<4>(p.ZZZ, W);
+  return r;
+}
+
+// madd-2008-s: P + (x2, y2); a must not be the identity; a.y QN (<= 4p)
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> r2_add_affine(const XYZZ<FpR2<Q>>& p, const Affine<FpR2<Q>>& a) {
+  using F = FpR2<Q>;
+  XYZZ<F> r;
+  if (fis_zero(p.ZZ)) {
+    r.X = a.x;
+    r.Y = a.y;
+    r.ZZ = F::one();
+    r.ZZZ = F::one();
+  } else {
+    const F U2 = r2_mul<4>(a.x, p.ZZ);
+    const F S2 = r2_mul<4>(a.y, p.ZZZ);
+    const F P = r2_sub<64>(U2, p.X);
+    const F R = r2_sub<16>(S2, p.Y);
+    const F PP = r2_sqr<256>(P);
+    const F RR = r2_sqr<64>(R);
+    const F PPP = r2_mul<4>(P, PP);
+    const F Qv = r2_mul<4>(p.X, PP);
+    r.ZZ = r2_mul<4>(p.ZZ, PP);
+    r.ZZZ = r2_mul<4>(p.ZZZ, PPP);
+    r.X = r2_sub3<16>(RR, PPP, Qv, Qv);
+    r.Y = r2_add(r2_mul<64>(r2_sub<64>(Qv, r.X), R), r2_mul<8>(p.Y, r2_neg<4>(PPP)));
+    if (r2_maybe_zero_prod(PP)) {  // rare: P = Q or P = -Q
+      const bool inf = r2_is_zero_prod(PP);
+      const bool dbl = inf && r2_is_zero_prod(RR);
+      XYZZ<F> d = xyzz_zero<F>();
+      if (dbl) d = r2_dbl_affine(a);
+      rr_sel(r, inf, d);
+    }
+  }
+  return r;
+}
+
+// add-2008-s: P + Q
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> r2_add_xyzz(const XYZZ<FpR2<Q>>& p, const XYZZ<FpR2<Q>>& q) {
+  using F = FpR2<Q>;
+  const bool pz = fis_zero(p.ZZ), qz = fis_zero(q.ZZ);
+  XYZZ<F> r;
+  if (pz || qz) {  // single exit, limb selects (see rr_sel)
+    r = q;
+    rr_sel(r, qz, p);
+  } else {
+    const F U1 = r2_mul<4>(p.X, q.ZZ);
+    const F U2 = r2_mul<4>(q.X, p.ZZ);
+    const F S1 = r2_mul<4>(p.Y, q.ZZZ);
+    const F S2 = r2_mul<4>(q.Y, p.ZZZ);
+    const F P = r2_sub<4>(U2, U1);
+    const F R = r2_sub<4>(S2, S1);
+    const F PP = r2_sqr<16>(P);
+    const F RR = r2_sqr<16>(R);
+    const F PPP = r2_mul<4>(P, PP);
+    const F Qv = r2_mul<4>(U1, PP);
+    r.ZZ = r2_mul<4>(r2_mul<4>(p.ZZ, q.ZZ), PP);
+    r.ZZZ = r2_mul<4>(r2_mul<4>(p.ZZZ, q.ZZZ), PPP);
+    r.X = r2_sub3<16>(RR, PPP, Qv, Qv);
+    r.Y = r2_add(r2_mul<16>(r2_sub<64>(Qv, r.X), R), r2_mul<8>(S1, r2_neg<4>(PPP)));
+    if (r2_maybe_zero_prod(PP)) {
+      const bool inf = r2_is_zero_prod(PP);
+      const bool dbl = inf && r2_is_zero_prod(RR);
+      XYZZ<F> d = xyzz_zero<F>();
+      if (dbl) d = r2_dbl(p);
+      rr_sel(r, inf, d);
+    }
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// point-arithmetic policy (curve_rr.hpp) for the Fq2 form
+// ---------------------------------------------------------------------------
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> pa_add_affine(const XYZZ<FpR2<Q>>& p, const Affine<FpR2<Q>>& a) {
+  return r2_add_affine(p, a);
+}
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> pa_add(const XYZZ<FpR2<Q>>& p, const XYZZ<FpR2<Q>>& q) {
+  return r2_add_xyzz(p, q);
+}
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> pa_dbl(const XYZZ<FpR2<Q>>& p) {
+  return r2_dbl(p);
+}
+template <class Q>
+ECG_DEV bool pa_is_zero(const XYZZ<FpR2<Q>>& p) {
+  return fis_zero(p.ZZ);
+}
+// -P: Y becomes 8p - Y (stored Y <= 4p; a negated Y <= 8p only meets
+// add-2008-s / dbl-2008-s-1 operands, whose K have the room)
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> pa_neg(const XYZZ<FpR2<Q>>& p) {
+  XYZZ<FpR2<Q>> r = p;
+  r.Y = r2_neg<8>(p.Y);
+  return r;
+}
+// negated base y, carried (QN): G2 products take no wide operand
+template <class Q>
+ECG_DEV FpR2<Q> pa_neg_y(const FpR2<Q>& y) {
+  return r2_neg<4>(y);
+}
+template <class Q>
+ECG_DEV XYZZ<Fp2<typename Q::Base>> pa_to_std(const XYZZ<FpR2<Q>>& p) {
+  if (fis_zero(p.ZZ)) return xyzz_zero<Fp2<typename Q::Base>>();
+  XYZZ<Fp2<typename Q::Base>> r;
+  r.X = rr2_to_std(p.X);
+  r.Y = rr2_to_std(p.Y);
+  r.ZZ = rr2_to_std(p.ZZ);
+  r.ZZZ = rr2_to_std(p.ZZZ);
+  return r;
+}
+
+// Coordinate field of the G2 bucket pipeline
+template <class C>
+constexpr bool has_rr2_form() {
+  return C::EXT == 2 && !std::is_same<typename RRof<typename C::FqParams>::Q, void>::value;
+}
+
+// ---------------------------------------------------------------------------
+// memory: an affine base is 4 NL words, an XYZZ point 8 NL words (16-B moves)
+// ---------------------------------------------------------------------------
+template <class Q>
+ECG_DEV Affine<FpR2<Q>> load_affine(const FpR2<Q>* xy) {
+  constexpr int NL = Q::NL;
+  uint32_t w[4 * NL];
+  rr_load_words<Q, 4 * NL>(xy, w);
+  Affine<FpR2<Q>> a;
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    a.x.c0.v[i] = w[i];
+    a.x.c1.v[i] = w[NL + i];
+    a.y.c0.v[i] = w[2 * NL + i];
+    a.y.c1.v[i] = w[3 * NL + i];
+  }
+  return a;
+}
+
+template <class Q>
+ECG_DEV void store_affine(FpR2<Q>* xy, const Affine<FpR2<Q>>& a) {
+  constexpr int NL = Q::NL;
+  uint32_t w[4 * NL];
+#pragma unroll
+  for (int i = 0; i < NL; i++) {
+    w[i] = a.x.c0.v[i];
+    w[NL + i] = a.x.c1.v[i];
+    w[2 * NL + i] = a.y.c0.v[i];
+    w[3 * NL + i] = a.y.c1.v[i];
+  }
+  rr_store_words<Q, 4 * NL>(xy, w);
+}
+
+template <class Q>
+ECG_DEV void rr_get_words(FpR<Q>& a, const uint32_t* w) {
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) a.v[i] = w[i];
+}
+template <class Q>
+ECG_DEV void rr_put_words(uint32_t* w, const FpR<Q>& a) {
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) w[i] = a.v[i];
+}
+
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> load_xyzz(const XYZZ<FpR2<Q>>* src) {
+  constexpr int NL = Q::NL;
+  uint32_t w[8 * NL];
+  rr_load_words<Q, 8 * NL>(src, w);
+  XYZZ<FpR2<Q>> p;
+  rr_get_words(p.X.c0, w);
+  rr_get_words(p.X.c1, w + NL);
+  rr_get_words(p.Y.c0, w + 2 * NL);
+  rr_get_words(p.Y.c1, w + 3 * NL);
+  rr_get_words(p.ZZ.c0, w + 4 * NL);
+  rr_get_words(p.ZZ.c1, w + 5 * NL);
+  rr_get_words(p.ZZZ.c0, w + 6 * NL);
+  rr_get_words(p.ZZZ.c1, w + 7 * NL);
+  return p;
+}
+
+template <class Q>
+ECG_DEV void store_xyzz(XYZZ<FpR2<Q>>* dst, const XYZZ<FpR2<Q>>& p) {
+  constexpr int NL = Q::NL;
+  uint32_t w[8 * NL];
+  rr_put_words(w, p.X.c0);
+  rr_put_words(w + NL, p.X.c1);
+  rr_put_words(w + 2 * NL, p.Y.c0);
+  rr_put_words(w + 3 * NL, p.Y.c1);
+  rr_put_words(w + 4 * NL, p.ZZ.c0);
+  rr_put_words(w + 5 * NL, p.ZZ.c1);
+  rr_put_words(w + 6 * NL, p.ZZZ.c0);
+  rr_put_words(w + 7 * NL, p.ZZZ.c1);
+  rr_store_words<Q, 8 * NL>(dst, w);
+}
+
+}  // namespace ecg

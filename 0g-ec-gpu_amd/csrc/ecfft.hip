@@ -31,7 +31,7 @@
 
 #include "ctx.hpp"
 #include "curve.hpp"
-#include "curve_rr.hpp"
+#include "curve_rr2.hpp"
 #include "dispatch.hpp"
 
 namespace ecg {
@@ -40,11 +40,19 @@ constexpr int ECFFT_THREADS = 64;
 
 
 // PF = coordinate field of the butterflies: C::Fq (32-bit limbs, lazy) or the
-// reduced-radix FpR of the G1 base fields (curve_rr.hpp)
+// reduced-radix FpR / FpR2 of the G1 / G2 base fields (curve_rr*.hpp)
 template <class C, class PF>
 ECG_DEV XYZZ<PF> to_pf(const XYZZ<typename C::Fq>& p) {
   if constexpr (std::is_same<PF, typename C::Fq>::value) {
     return p;
+  } else if constexpr (C::EXT == 2) {
+    using Q = typename PF::Params;
+    XYZZ<PF> r;
+    r.X = rr2_from_std<Q>(p.X);
+    r.Y = rr2_from_std<Q>(p.Y);
+    r.ZZ = rr2_from_std<Q>(p.ZZ);
+    r.ZZZ = rr2_from_std<Q>(p.ZZZ);
+    return r;
   } else {
     return pa_from_std_rr<typename PF::Params>(p);
   }
@@ -255,6 +263,10 @@ static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t lo
   if constexpr (has_rr_form<C>()) {
     if (ecfft_rr_enabled())
       return ecfft_pf<C, FpR<typename RRof<typename C::FqParams>::Q>>(ctx, d_jac, omega, log_n, s, abort_cb, user);
+  }
+  if constexpr (has_rr2_form<C>()) {
+    if (ecfft_rr_enabled())
+      return ecfft_pf<C, FpR2<typename RRof<typename C::FqParams>::Q>>(ctx, d_jac, omega, log_n, s, abort_cb, user);
   }
   return ecfft_pf<C, typename C::Fq>(ctx, d_jac, omega, log_n, s, abort_cb, user);
 }

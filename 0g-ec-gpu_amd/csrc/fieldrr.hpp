@@ -476,8 +476,8 @@ ECG_DEV FpR<Q> rr_add(const FpR<Q>& a, const FpR<Q>& b) {
 
 template <int K>
 constexpr int kp_index() {
-  static_assert(K >= 2 && (K & (K - 1)) == 0 && K <= 64, "k must be a power of two in [2, 64]");
-  return K == 2 ? 0 : K == 4 ? 1 : K == 8 ? 2 : K == 16 ? 3 : K == 32 ? 4 : 5;
+  static_assert(K >= 2 && (K & (K - 1)) == 0 && K <= 256, "k must be a power of two in [2, 256]");
+  return K == 2 ? 0 : K == 4 ? 1 : K == 8 ? 2 : K == 16 ? 3 : K == 32 ? 4 : K == 64 ? 5 : K == 128 ? 6 : 7;
 }
 
 // a - b + K p  (requires value(b) <= K p / 2)

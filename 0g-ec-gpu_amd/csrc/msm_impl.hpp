@@ -51,7 +51,7 @@
 
 #include "ctx.hpp"
 #include "curve.hpp"
-#include "curve_rr.hpp"
+#include "curve_rr2.hpp"
 #include "dispatch.hpp"
 #include "host_field.hpp"
 
@@ -155,15 +155,20 @@ struct MsmGeom {
 // run two 128-step chains while the others idle for the second.  Below
 // MSM_RED_THREADS segments (2 waves on each of the 1024 SIMDs) the groups'
 // buckets are therefore cut into exactly that many equal segments (any
-// length: the offset kernel multiplies by the segment's first index).
+// length: the offset kernel multiplies by the segment's first index).  The
+// target is one round of `waves` waves per SIMD -- the reduction kernels'
+// occupancy (RedWaves): 2 for reduced-radix G1 points, 1 for G2, whose second
+// round of segments would only double the offset kernel's scalar products
+// (G2 2^22: msm_reduce_offset 2.1 ms at 2 rounds).
 // ECG_MSM_RED_SEG pins LS (A/B).
 constexpr uint32_t MSM_RED_THREADS = 2 * 1024 * 64;
-static void plan_reduction(MsmPlan& pl) {
+static void plan_reduction(MsmPlan& pl, uint32_t waves = 2) {
+  const uint32_t target = MSM_RED_THREADS / 2 * waves;
   uint32_t ls = msm_red_seg();
   if (!ls) {
     ls = 64;
-    if ((double)pl.G * pl.B / 64 < MSM_RED_THREADS) {
-      const uint32_t per_group = std::max(1u, MSM_RED_THREADS / pl.G);
+    if ((double)pl.G * pl.B / 64 < target) {
+      const uint32_t per_group = std::max(1u, target / pl.G);
       ls = (pl.B + per_group - 1) / per_group;
     }
   }
@@ -373,6 +378,10 @@ template <class Q>
 struct BaseLayout<FpR<Q>> {
   static constexpr size_t BYTES = (2 * sizeof(FpR<Q>) + 127) / 128 * 128;
 };
+template <class Q>
+struct BaseLayout<FpR2<Q>> {  // G2: 4 NL words (224 B / 160 B) in two 128-B lines
+  static constexpr size_t BYTES = (2 * sizeof(FpR2<Q>) + 127) / 128 * 128;
+};
 template <class F>
 ECG_HD const F* base_ptr(const F* bases, size_t i) {
   return reinterpret_cast<const F*>(reinterpret_cast<const char*>(bases) + i * BaseLayout<F>::BYTES);
@@ -391,6 +400,10 @@ ECG_DEV void limb_sel(Fp<P>& r, bool c, const Fp<P>& s) {
 }
 template <class Q>
 ECG_DEV void limb_sel(FpR<Q>& r, bool c, const FpR<Q>& s) {
+  rr_sel(r, c, s);
+}
+template <class Q>
+ECG_DEV void limb_sel(FpR2<Q>& r, bool c, const FpR2<Q>& s) {
   rr_sel(r, c, s);
 }
 template <class P>
@@ -699,29 +712,43 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
 // reduced-radix pipeline (curve_rr.hpp): bases into the R' form before step 3,
 // window sums back to the 32-bit-limb form after step 6
 // ---------------------------------------------------------------------------
+// boundary field of a pipeline field, and the conversion into it
+template <class AF>
+struct StdOf;
 template <class Q>
+struct StdOf<FpR<Q>> {
+  using type = Fp<typename Q::Base>;
+  static ECG_DEV FpR<Q> conv(const type& a) { return rr_from_std<Q>(a); }
+};
+template <class Q>
+struct StdOf<FpR2<Q>> {
+  using type = Fp2<typename Q::Base>;
+  static ECG_DEV FpR2<Q> conv(const type& a) { return rr2_from_std<Q>(a); }
+};
+
+template <class AF>
 __global__ void __launch_bounds__(MSM_THREADS)
-    msm_rr_bases_kernel(const Fp<typename Q::Base>* __restrict__ in, size_t n, uint32_t stride,
-                        FpR<Q>* __restrict__ out) {
-  using F = Fp<typename Q::Base>;
+    msm_rr_bases_kernel(const typename StdOf<AF>::type* __restrict__ in, size_t n, uint32_t stride,
+                        AF* __restrict__ out) {
+  using F = typename StdOf<AF>::type;
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const Affine<F> a = load_affine(in + 2 * i);
-  Affine<FpR<Q>> r;
+  Affine<AF> r;
   if (aff_is_identity(a)) {  // GpuRepr identity stays all-zero (impls.rs:52-54)
-    r.x = FpR<Q>::zero();
-    r.y = FpR<Q>::zero();
+    r.x = AF::zero();
+    r.y = AF::zero();
   } else {
-    r.x = rr_from_std<Q>(a.x);
-    r.y = rr_from_std<Q>(a.y);
+    r.x = StdOf<AF>::conv(a.x);
+    r.y = StdOf<AF>::conv(a.y);
   }
-  FpR<Q>* rec = base_ptr(out, i * stride);  // stride > 1: one row of an interleaved window table
+  AF* rec = base_ptr(out, i * stride);  // stride > 1: one row of an interleaved window table
   store_affine(rec, r);
   // zero the record's pad too: whole-line writes (a partial line costs a
   // read-modify-write; measured 3.3 -> 5.6 ms for this kernel without it)
-  constexpr size_t pad = BaseLayout<FpR<Q>>::BYTES - 2 * sizeof(FpR<Q>);
+  constexpr size_t pad = BaseLayout<AF>::BYTES - 2 * sizeof(AF);
   static_assert(pad % 16 == 0, "16-B vector stores");
-  uint4* tail = reinterpret_cast<uint4*>(reinterpret_cast<char*>(rec) + 2 * sizeof(FpR<Q>));
+  uint4* tail = reinterpret_cast<uint4*>(reinterpret_cast<char*>(rec) + 2 * sizeof(AF));
 #pragma unroll
   for (size_t k = 0; k < pad / 16; k++) tail[k] = make_uint4(0, 0, 0, 0);
 }
@@ -737,6 +764,16 @@ static bool msm_rr_enabled() {  // A/B switch: ECG_MSM_RR=0 runs the 32-bit-limb
   static const bool v = env_u32("ECG_MSM_RR", 1) != 0;
   return v;
 }
+
+// Coordinate field of the bucket pipeline: the reduced-radix Fq (G1) or Fq2
+// (G2) form, else the boundary field (curves without an rr layout).
+template <class C>
+struct MsmField {
+  using Q = typename RRof<typename C::FqParams>::Q;
+  static constexpr bool rr = has_rr_form<C>() || has_rr2_form<C>();
+  using type = std::conditional_t<has_rr_form<C>(), FpR<Q>,
+                                  std::conditional_t<has_rr2_form<C>(), FpR2<Q>, typename C::Fq>>;
+};
 
 // ---------------------------------------------------------------------------
 // Synthetic bases P_i = (a + i*b) G  (bench/test input generator)
@@ -853,9 +890,11 @@ static inline uint32_t blocks_for(size_t n, int threads) { return (uint32_t)((n 
 // (msm_prepare_t), so the per-call conversion is skipped.
 template <class C, class AF>
 int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
-                  const MsmPlan& pl, hipStream_t s, void** d_sums, bool prepared) {
+                  const MsmPlan& pl0, hipStream_t s, void** d_sums, bool prepared) {
   using F = AF;
   using X = XYZZ<F>;
+  MsmPlan pl = pl0;  // reduction segments sized for this point form's occupancy
+  plan_reduction(pl, RedWaves<F>::value);
   const size_t m = (size_t)g.n_chunks * g.clen;  // scalars consumed
   const uint32_t nb = pl.G * pl.B;
   const uint32_t sentinel = nb;
@@ -897,7 +936,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     if (!prepared) {
       void* rb;
       ECG_TRY(ws_get(ctx, "msm_rr_bases", nb_in * BaseLayout<F>::BYTES, &rb));
-      hipLaunchKernelGGL(msm_rr_bases_kernel<typename F::Params>, dim3(blocks_for(nb_in, MSM_THREADS)),
+      hipLaunchKernelGGL(msm_rr_bases_kernel<F>, dim3(blocks_for(nb_in, MSM_THREADS)),
                          dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, nb_in, 1u, (F*)rb);
       ECG_HIP(hipGetLastError());
       bases = (const F*)rb;
@@ -1002,10 +1041,9 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
 template <class C>
 int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g, const MsmPlan& pl,
                hipStream_t s, void** d_sums, bool prepared = false) {
-  if constexpr (has_rr_form<C>()) {
+  if constexpr (MsmField<C>::rr) {
     if (msm_rr_enabled())
-      return msm_core_impl<C, FpR<typename RRof<typename C::FqParams>::Q>>(ctx, d_bases, d_scalars, g, pl, s,
-                                                                            d_sums, prepared);
+      return msm_core_impl<C, typename MsmField<C>::type>(ctx, d_bases, d_scalars, g, pl, s, d_sums, prepared);
   }
   return msm_core_impl<C, typename C::Fq>(ctx, d_bases, d_scalars, g, pl, s, d_sums, prepared);
 }
@@ -1014,8 +1052,8 @@ int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const M
 // (G1) or the [x, y] boundary layout (G2, or ECG_MSM_RR=0).
 template <class C>
 size_t msm_base_record_bytes() {
-  if constexpr (has_rr_form<C>()) {
-    if (msm_rr_enabled()) return BaseLayout<FpR<typename RRof<typename C::FqParams>::Q>>::BYTES;
+  if constexpr (MsmField<C>::rr) {
+    if (msm_rr_enabled()) return BaseLayout<typename MsmField<C>::type>::BYTES;
   }
   return 2 * sizeof(typename C::Fq);
 }
@@ -1102,10 +1140,10 @@ __global__ void __launch_bounds__(MSM_THREADS)
 // one row of an interleaved window table).
 template <class C>
 int msm_records_t(const void* d_bases, size_t n, void* d_out, hipStream_t s, uint32_t stride = 1) {
-  if constexpr (has_rr_form<C>()) {
+  if constexpr (MsmField<C>::rr) {
     if (msm_rr_enabled()) {
-      using AF = FpR<typename RRof<typename C::FqParams>::Q>;
-      hipLaunchKernelGGL(msm_rr_bases_kernel<typename AF::Params>, dim3(blocks_for(n, MSM_THREADS)),
+      using AF = typename MsmField<C>::type;
+      hipLaunchKernelGGL(msm_rr_bases_kernel<AF>, dim3(blocks_for(n, MSM_THREADS)),
                          dim3(MSM_THREADS), 0, s, (const typename C::Fq*)d_bases, n, stride, (AF*)d_out);
       ECG_HIP(hipGetLastError());
       return ECG_OK;
@@ -1212,8 +1250,8 @@ template <class C>
 size_t msm_pass_terms(const ecg_ctx* ctx) {
   if (ctx->msm_chunk) return ctx->msm_chunk;
   using F = typename C::Fq;
-  constexpr bool rr = has_rr_form<C>();
-  using AF = std::conditional_t<rr, FpR<typename RRof<typename C::FqParams>::Q>, F>;
+  constexpr bool rr = MsmField<C>::rr;
+  using AF = typename MsmField<C>::type;
   const MsmPlan pl = make_plan((size_t)1 << 26, (uint32_t)C::FrParams::BITS);
   const double per_term = 2.0 * sizeof(F) + 32.0 + (rr ? (double)BaseLayout<AF>::BYTES : 0.0) + 16.0 * pl.W +
                           2.0 * pl.W / pl.seg * (sizeof(XYZZ<AF>) + 4) * (1.0 + 1.0 / 16);

@@ -10,6 +10,9 @@
 //   add      v_add_u32 (plain 32-bit op)
 //   add64    v_lshl_add_u64 (64-bit add, shift 0)
 //   bfe      v_alignbit_b32 (radix-change helper)
+//   and the other non-MAD ops of the reduced-radix products: 64-bit shift,
+//   and/sub/shift/mov (32-bit), cndmask with an SGPR mask, mad with an SGPR
+//   operand, and_or
 // Build: hipcc --offload-arch=gfx950 -O3 -o issue_bench issue_bench.hip
 #include <hip/hip_runtime.h>
 
@@ -42,6 +45,14 @@ constexpr int ITERS = 2048;
 #define ADD(i) "v_add_u32 %[t" #i "], %[t" #i "], %[x]\n\t"
 #define ADD64(i) "v_lshl_add_u64 %[a" #i "], %[a" #i "], 0, %[a" #i "]\n\t"
 #define BFE(i) "v_alignbit_b32 %[t" #i "], %[t" #i "], %[x], 29\n\t"
+#define SHR64(i) "v_lshrrev_b64 %[a" #i "], 29, %[a" #i "]\n\t"
+#define AND(i) "v_and_b32 %[t" #i "], %[t" #i "], %[x]\n\t"
+#define SUB(i) "v_sub_u32 %[t" #i "], %[t" #i "], %[x]\n\t"
+#define SHR32(i) "v_lshrrev_b32 %[t" #i "], 29, %[t" #i "]\n\t"
+#define MOV(i) "v_mov_b32 %[t" #i "], %[x]\n\t"
+#define CND64(i) "v_cndmask_b32_e64 %[t" #i "], %[t" #i "], %[x], s[40:41]\n\t"
+#define MADS(i) "v_mad_u64_u32 %[a" #i "], s[40:41], %[x], s44, %[a" #i "]\n\t"
+#define ANDOR(i) "v_and_or_b32 %[t" #i "], %[t" #i "], %[x], %[y]\n\t"
 #define X8(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7)
 
 #define KERNEL(NAME, BODY)                                                                         \
@@ -83,6 +94,14 @@ KERNEL(k_cnd, X8(CND))
 KERNEL(k_fma64, X8(FMA64))
 KERNEL(k_add64, X8(ADD64))
 KERNEL(k_bfe, X8(BFE))
+KERNEL(k_shr64, X8(SHR64))
+KERNEL(k_and, X8(AND))
+KERNEL(k_sub, X8(SUB))
+KERNEL(k_shr32, X8(SHR32))
+KERNEL(k_mov, X8(MOV))
+KERNEL(k_cnd64, X8(CND64))
+KERNEL(k_mads, X8(MADS))
+KERNEL(k_andor, X8(ANDOR))
 
 typedef void (*kern_t)(uint64_t*, uint32_t);
 
@@ -94,6 +113,9 @@ int main() {
       {"add_co_e32", k_addco, 16}, {"add3", k_add3, 16}, {"mul_u32_u24", k_mul24, 16},
       {"mul_hi_u24", k_mulhi24, 16}, {"mul_lo_u32", k_mullo, 16}, {"mul_hi_u32", k_mulhi, 16},
       {"cndmask_e32", k_cnd, 16}, {"fma_f64", k_fma64, 16},
+      {"lshrrev_b64", k_shr64, 16}, {"and_b32", k_and, 16}, {"sub_u32", k_sub, 16}, {"lshrrev_b32", k_shr32, 16},
+      {"mov_b32", k_mov, 16}, {"cndmask_e64 sgpr", k_cnd64, 16}, {"mad sgpr operand", k_mads, 16},
+      {"and_or_b32", k_andor, 16},
   };
   uint64_t* out;
   CHK(hipMalloc(&out, sizeof(uint64_t) << 24));
@@ -101,7 +123,7 @@ int main() {
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
   int ncu = 256;
-  for (int wps : {2, 8}) {
+  for (int wps : {2, 4}) {
     const int blocks = ncu * wps, threads = 256;  // 256 threads = 1 wave per SIMD per block
     for (auto& k : ks) {
       float best = 1e30f;
