@@ -107,3 +107,34 @@ def test_g2_ec_fft_linearity(gpu_programs, cname, cid, cv):
     fs = po.serial_fft([(a + j * b) % r for j in range(n)], w, log_n, r)
     for kk in (0, 1, 2, 100, n - 1):
         assert to_py_affine(cv, jac[kk]) == po.g2_to_affine(cv, po.g2_scalar_mul(cv, cv.gen, fs[kk])), kk
+
+
+@pytest.mark.parametrize("cname,cid,cv", G2)
+def test_g2_msm_exceptional_paths(gpu_programs, cname, cid, cv):
+    """Equal bases drive the doubling branch of the mixed add (acc = P, + P)
+    and of the full add in the combine / reduction (k P + k P); a base next to
+    its negative drives the P + (-P) = O branch.  The reduced-radix Fq2 form
+    detects both on PP's components (curve_rr2.hpp); random inputs never do."""
+    prog = gpu_programs[0][0]
+    p = cv.fq.modulus
+    r = cv.fr.modulus
+    k0 = 0xC0FFEE
+    P = po.g2_to_affine(cv, po.g2_scalar_mul(cv, cv.gen, k0))
+    row = np.array(fq2_limbs(cv, P[0]) + fq2_limbs(cv, P[1]), dtype=np.uint64)
+    nrow = np.array(fq2_limbs(cv, P[0]) + fq2_limbs(cv, po.Fq2(0, 0, p) - P[1]), dtype=np.uint64)
+    rng = np.random.default_rng(7 + cid)
+    for n in (64, 1 << 16):
+        B = np.ascontiguousarray(np.tile(row, (n, 1)))
+        E = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+        E[:, 3] &= np.uint64((1 << (cv.fr.bits - 192 - 1)) - 1)
+        d_b = ecgpu.DeviceBuffer.upload(prog, B)
+        d_e = ecgpu.DeviceBuffer.upload(prog, E)
+        got = to_py_affine(cv, ecgpu.msm_dev(prog, cname, d_b, d_e, n))
+        s = sum(po.limbs_to_int(e) for e in E) % r
+        assert got == po.g2_to_affine(cv, po.g2_scalar_mul(cv, cv.gen, s * k0 % r)), n
+        # equal scalars, one base and its negative alternating: every bucket cancels
+        Bn = np.ascontiguousarray(np.where((np.arange(n) % 2 == 1)[:, None], nrow, row))
+        Ee = np.ascontiguousarray(np.tile(E[0], (n, 1)))
+        d_b = ecgpu.DeviceBuffer.upload(prog, Bn)
+        d_e = ecgpu.DeviceBuffer.upload(prog, Ee)
+        assert to_py_affine(cv, ecgpu.msm_dev(prog, cname, d_b, d_e, n)) is None, n
