@@ -346,3 +346,28 @@ def test_msm_skewed_scalars_2p22(gpu_programs, pattern):
     kat = co.kat_scalar(0, a, b, E, nthreads=16)
     assert same_point(0, out, co.gen_mul(0, kat))
     assert dt < 5.0, dt
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_equal_and_opposite_bases(gpu_programs, cname, cid):
+    """Every base equal (mixed-add and full-add doublings in every bucket,
+    record and reduction level) and a base beside its negative with equal
+    scalars (every bucket cancels): the exceptional branches of the reduced-
+    radix formulas (curve_rr.hpp), which random inputs never reach."""
+    prog = gpu_programs[0][0]
+    cv = po.CURVES[cname]
+    r = cv.fr.modulus
+    k0 = 0xC0FFEE
+    rng = np.random.default_rng(11 + cid)
+    row, nrow = co.gen_bases(cid, k0, 1, 1)[0], co.gen_bases(cid, r - k0, 1, 1)[0]  # P = k0 G, -P
+    for n in (64, 1 << 16):
+        B = np.ascontiguousarray(np.tile(row, (n, 1)))
+        E = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+        E[:, 3] &= np.uint64((1 << (cv.fr.bits - 192 - 1)) - 1)
+        out = ecgpu.msm_dev(prog, cname, ecgpu.DeviceBuffer.upload(prog, B), ecgpu.DeviceBuffer.upload(prog, E), n)
+        s = sum(po.limbs_to_int(e) for e in E) % r
+        assert same_point(cid, out, co.gen_mul(cid, s * k0 % r)), n
+        Bn = np.ascontiguousarray(np.where((np.arange(n) % 2 == 1)[:, None], nrow, row))
+        Ee = np.ascontiguousarray(np.tile(E[0], (n, 1)))
+        out = ecgpu.msm_dev(prog, cname, ecgpu.DeviceBuffer.upload(prog, Bn), ecgpu.DeviceBuffer.upload(prog, Ee), n)
+        assert aff(cid, out) is None, n
