@@ -195,6 +195,152 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
   store_xyzz(&a[i1], pa_add(A, pa_neg(B)));
 }
 
+// ---------------------------------------------------------------------------
+// Windowed stage (default): the butterflies of the small transforms 0g runs
+// (2^10..2^16 points: 512..32768 butterflies, under one wave per SIMD) are
+// latency-bound -- a stage takes one scalar multiplication's dependency chain,
+// whatever the lane count -- so the stage shortens the chain:
+//  * signed 4-bit windows with no carry pass: K = k + sum_i 8 * 16^i, digit i
+//    = nibble i of K minus 8, in [-8, 7]; a table m P (m = 1..8, 4 levels of
+//    adds/doublings) in the lane's global slot; per digit 4 doublings and one
+//    add (15/16 of digits are nonzero): 128 doublings + 32 adds per 128 bits
+//    instead of the bit ladder's 128 + 64 (+ 96 for the joint GLV ladder);
+//  * on GLV curves two lanes per butterfly, one per half (k1 P and k2 phi(P)),
+//    joined by a lane shuffle and one add: the joint ladder's 128 doublings
+//    + ~96 adds become 128 doublings + ~34 adds on the critical path.
+// ---------------------------------------------------------------------------
+constexpr int ECFFT_TAB = 8;  // table entries per lane (m P, m = 1..8)
+
+// r.Y = -r.Y where c, word by word (no whole-struct copy under a condition)
+template <class PF>
+ECG_DEV XYZZ<PF> neg_if(const XYZZ<PF>& p, bool c) {
+  const XYZZ<PF> n = pa_neg(p);
+  constexpr int NW = (int)(sizeof(PF) / 4);
+  uint32_t w[NW], nw[NW];
+  __builtin_memcpy(w, &p.Y, sizeof(PF));
+  __builtin_memcpy(nw, &n.Y, sizeof(PF));
+#pragma unroll
+  for (int i = 0; i < NW; i++) w[i] = c ? nw[i] : w[i];
+  XYZZ<PF> r = p;
+  __builtin_memcpy(&r.Y, w, sizeof(PF));
+  return r;
+}
+
+template <class T>
+ECG_DEV T sel_words(bool c, const T& a, const T& b) {  // c ? a : b
+  constexpr int NW = (int)(sizeof(T) / 4);
+  uint32_t wa[NW], wb[NW];
+  __builtin_memcpy(wa, &a, sizeof(T));
+  __builtin_memcpy(wb, &b, sizeof(T));
+#pragma unroll
+  for (int i = 0; i < NW; i++) wb[i] = c ? wa[i] : wb[i];
+  T r;
+  __builtin_memcpy(&r, wb, sizeof(T));
+  return r;
+}
+
+template <class T>
+ECG_DEV T shfl_xor1(const T& v) {  // the partner lane's value (lanes 2u <-> 2u + 1)
+  constexpr int NW = (int)(sizeof(T) / 4);
+  uint32_t w[NW];
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (int i = 0; i < NW; i++) w[i] = (uint32_t)__shfl_xor((int)w[i], 1);
+  T r;
+  __builtin_memcpy(&r, w, sizeof(T));
+  return r;
+}
+
+// k P, k little-endian in W words (signed 4-bit windows, see above)
+template <int W, class PF>
+ECG_DEV XYZZ<PF> win_mul(const XYZZ<PF>& P, const uint32_t* k, XYZZ<PF>* __restrict__ tab) {
+  uint32_t K[W + 1];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    c += (uint64_t)k[i] + 0x88888888u;
+    K[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  K[W] = (uint32_t)c + 8u;  // digit 8W in {0, 1}
+  // table m P, m = 1..8: four levels (2P; 3P, 4P; 5P, 6P, 8P; 7P)
+  store_xyzz(&tab[0], P);
+  const XYZZ<PF> P2 = pa_dbl(P);
+  store_xyzz(&tab[1], P2);
+  const XYZZ<PF> P3 = pa_add(P2, P);
+  store_xyzz(&tab[2], P3);
+  const XYZZ<PF> P4 = pa_dbl(P2);
+  store_xyzz(&tab[3], P4);
+  store_xyzz(&tab[4], pa_add(P4, P));
+  const XYZZ<PF> P6 = pa_dbl(P3);
+  store_xyzz(&tab[5], P6);
+  store_xyzz(&tab[6], pa_add(P6, P));
+  store_xyzz(&tab[7], pa_dbl(P4));
+  XYZZ<PF> acc = xyzz_zero<PF>();
+#pragma unroll 1
+  for (int i = 8 * W; i >= 0; i--) {
+    uint32_t word = K[0];
+#pragma unroll
+    for (int q = 1; q <= W; q++) word = (i >> 3) == q ? K[q] : word;
+    const int d = (int)((word >> ((i & 7) * 4)) & 15u) - 8;
+    const XYZZ<PF> T = load_xyzz(&tab[d < 0 ? -d - 1 : d > 0 ? d - 1 : 0]);  // issued before the doublings
+#pragma unroll 1
+    for (int b = 0; b < 4; b++) acc = pa_dbl(acc);
+    if (d != 0) acc = pa_add(acc, neg_if(T, d < 0));
+  }
+  return acc;
+}
+
+// Stage s (as ecfft_stage_kernel) with windowed products; GLV curves: lanes
+// 2u, 2u + 1 share butterfly u (half 0: k1 P, half 1: k2 phi(P)).
+template <class C, class PF>
+__global__ void __launch_bounds__(ECFFT_THREADS)
+    ecfft_stage_win_kernel(XYZZ<PF>* __restrict__ a, const uint4* __restrict__ tw, uint32_t log_n, uint32_t s,
+                           XYZZ<PF>* __restrict__ tabs) {
+  constexpr bool glv = has_glv<C>();
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = glv ? g >> 1 : g;
+  const uint32_t half = glv ? (g & 1) : 0u;
+  if (t >= (1u << (log_n - 1))) return;  // both lanes of a pair leave together
+  const uint32_t h = 1u << s;
+  const uint32_t j = t & (h - 1);
+  const uint32_t i0 = ((t >> s) << (s + 1)) + j, i1 = i0 + h;
+  const XYZZ<PF> A = load_xyzz(&a[i0]);
+  const XYZZ<PF> B = load_xyzz(&a[i1]);
+  XYZZ<PF> R = B;
+  if (j != 0) {  // uniform within a pair
+    const uint32_t e = j << (log_n - 1 - s);
+    if constexpr (glv) {
+      const uint4 kk = tw[2 * e + half];
+      const uint32_t k[4] = {kk.x, kk.y, kk.z, kk.w};
+      typename C::Fq beta;
+      from_u64_words(beta, C::Gen::BETA);
+      XYZZ<PF> Bh = B;
+      Bh.X = sel_words(half != 0, pa_mul_const(B.X, beta), B.X);  // phi(x, y) = (beta x, y)
+      const XYZZ<PF> Rh = win_mul<4>(Bh, k, tabs + (size_t)ECFFT_TAB * g);
+      R = pa_add(Rh, shfl_xor1(Rh));
+    } else {
+      const uint4 lo = tw[2 * e], hi = tw[2 * e + 1];
+      const uint32_t k[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      R = win_mul<8>(B, k, tabs + (size_t)ECFFT_TAB * g);
+    }
+  }
+  if constexpr (glv) {  // lane 0 writes A + wB, lane 1 A - wB
+    store_xyzz(&a[half ? i1 : i0], pa_add(A, neg_if(R, half != 0)));
+  } else {
+    store_xyzz(&a[i0], pa_add(A, R));
+    store_xyzz(&a[i1], pa_add(A, pa_neg(R)));
+  }
+}
+
+static bool ecfft_win_enabled() {  // A/B switch: ECG_ECFFT_WIN=0 keeps the bit ladders (ecfft_stage_kernel)
+  static const bool v = [] {
+    const char* e = getenv("ECG_ECFFT_WIN");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <class C, class PF>
 __global__ void __launch_bounds__(ECFFT_THREADS)
     ecfft_store_kernel(const XYZZ<PF>* __restrict__ a, uint32_t n, typename C::Fq* __restrict__ jac) {
@@ -228,7 +374,14 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
   void *a, *tw, *gt = nullptr;
   ECG_TRY(ws_get(ctx, "ecfft_pts", (size_t)n * sizeof(XYZZ<PF>), &a));
   ECG_TRY(ws_get(ctx, "ecfft_tw", (size_t)(n / 2 + 1) * 32, &tw));
-  if (has_glv<C>()) ECG_TRY(ws_get(ctx, "ecfft_glv", (size_t)(n / 2 + 1) * 3 * sizeof(XYZZ<PF>), &gt));
+  // windowed stages for the reduced-radix point forms (the 32-bit-limb forms
+  // are the A/B baseline and keep the bit ladders)
+  const bool win = !std::is_same<PF, F>::value && ecfft_win_enabled();
+  const size_t lanes = has_glv<C>() && win ? n : n / 2 + 1;  // stage lanes (2 per butterfly on GLV curves)
+  if (win)
+    ECG_TRY(ws_get(ctx, "ecfft_tab", lanes * ECFFT_TAB * sizeof(XYZZ<PF>), &gt));
+  else if (has_glv<C>())
+    ECG_TRY(ws_get(ctx, "ecfft_glv", (size_t)(n / 2 + 1) * 3 * sizeof(XYZZ<PF>), &gt));
   S om;
   memcpy(om.v, omega, sizeof(om.v));
   hipLaunchKernelGGL((ecfft_load_kernel<C, PF>), dim3(ecfft_blocks(n)), dim3(ECFFT_THREADS), 0, s, (const F*)d_jac, log_n,
@@ -246,8 +399,14 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
       return ECG_ABORTED;
     }
     ECG_TRY(kt_begin(ctx, "ecfft_stage", s));
-    hipLaunchKernelGGL((ecfft_stage_kernel<C, PF>), dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s,
-                       (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, (XYZZ<PF>*)gt);
+    if constexpr (!std::is_same<PF, F>::value) {
+      if (win)
+        hipLaunchKernelGGL((ecfft_stage_win_kernel<C, PF>), dim3(ecfft_blocks(has_glv<C>() ? n : n / 2)),
+                           dim3(ECFFT_THREADS), 0, s, (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, (XYZZ<PF>*)gt);
+    }
+    if (!win)
+      hipLaunchKernelGGL((ecfft_stage_kernel<C, PF>), dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s,
+                         (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, (XYZZ<PF>*)gt);
     ECG_HIP(hipGetLastError());
     ECG_TRY(kt_end(ctx, "ecfft_stage", s));
   }
