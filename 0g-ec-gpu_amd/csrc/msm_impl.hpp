@@ -90,6 +90,10 @@ static bool msm_pw_enabled() {  // A/B switch: ECG_MSM_PW=0 keeps one global sor
   static const bool v = env_u32("ECG_MSM_PW", 1) != 0;
   return v;
 }
+static bool msm_pw_one_enabled() {  // A/B switch: ECG_MSM_PW1=0 sorts every block on its own
+  static const bool v = env_u32("ECG_MSM_PW1", 1) != 0;
+  return v;
+}
 static int msm_sort_cfg() {  // onesweep config of the per-block sorts (A/B: ECG_MSM_SORTCFG)
   static const int v = (int)env_u32("ECG_MSM_SORTCFG", 2);
   return v;
@@ -951,9 +955,19 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   // (an MSD counting sort with 10-bit coarse bins was measured 3x slower:
   // 13K bins leave ~0.15 entries per bin per tile, so its scatter cannot
   // coalesce -- onesweep's 8-bit digits exist for exactly that reason)
+  // Window-padded keys whose window id and local key fit 20 bits together
+  // (c <= 16 with 16 windows: up to 2^22 terms) are sorted in ONE 2-pass
+  // sort over every block: the blocks already sit in window order and carry
+  // the window in the key's high bits, so the stable sort leaves each block
+  // where it was and yields exactly the per-block result.  Per-block sorts
+  // of <= 2^22 entries took rocPRIM's small-input path (10 launches per block
+  // at 2^20: 2.7 of the 7.1 ms MSM) or onesweep launch tails.
+  uint32_t wbits = 0;
+  while ((1u << wbits) < line_groups) wbits++;
+  const bool pw_one = pw && msm_pw_one_enabled() && pl.c + wbits <= 20;
   const int cfg = pw ? msm_sort_cfg() : 0;
-  const size_t sort_n = pw ? mpad : total;  // one sort per block, or one global sort
-  const int sort_bits = pw ? (int)pl.c : key_bits;
+  const size_t sort_n = pw && !pw_one ? mpad : total;  // one sort per block, or one sort of all blocks
+  const int sort_bits = pw ? (int)(pw_one ? pl.c + wbits : pl.c) : key_bits;
   size_t tmp_bytes = 0;
   ECG_HIP(msm_sort(cfg, nullptr, tmp_bytes, (uint64_t*)e0, (uint64_t*)e1, sort_n, 0, sort_bits, s));
   ECG_TRY(ws_get(ctx, "msm_sort_tmp", tmp_bytes, &tmp));
