@@ -419,6 +419,23 @@ def main():
     aux = None
     if rank == 0 and world == 1 and not args.no_aux:
         aux = {}
+        # BASELINE config 3: G1 MSM at 2^20 -- the first 2^20 resident terms, KAT-checked
+        n20 = 1 << 20
+        if n_loc >= n20:
+            ecgpu.msm_dev(prog, args.curve, d_msm_bases, d_scal, n20)
+            best20 = 1e9
+            for _ in range(5):
+                t_a = time.perf_counter()
+                out20 = ecgpu.msm_dev(prog, args.curve, d_msm_bases, d_scal, n20)
+                best20 = min(best20, time.perf_counter() - t_a)
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import coracle as co20
+            k20 = co20.kat_scalar(cid, a_loc, KAT_B, scal[:n20], nthreads=nthreads) % r_int
+            want20 = co20.jac_to_affine(cid, co20.gen_mul(cid, k20))
+            got20 = co20.jac_to_affine(cid, out20)
+            aux["msm_2p20"] = {"ms": best20 * 1e3, "point_adds_per_s": n20 / best20,
+                               "kat": bool(want20 is not None and got20 is not None and (want20 == got20).all()),
+                               "note": "BASELINE config 3: first 2^20 resident terms, best of 5 synchronous calls"}
         # batched multi-line MSM on the ag-cuda-ec AMT shape (benches/amt.rs: LOG_N=10 -> 2^21 x 10 lines)
         L, lines, chunks = 1 << 21, 10, 1 << 10
         d_lb = ecgpu.gen_bases_dev(prog, args.curve, 7, 11, L * lines)
