@@ -174,15 +174,22 @@ static void plan_reduction(MsmPlan& pl, uint32_t waves = 2) {
     if ((double)pl.G * pl.B / 64 < target) {
       const uint32_t per_group = std::max(1u, target / pl.G);
       ls = (pl.B + per_group - 1) / per_group;
+      // a few hundred thousand buckets cut into chains shorter than 8 spend
+      // more on the per-segment offsets (~1.5 log2 B point ops each) than on
+      // the running sums: one wave per SIMD of 8-bucket chains is faster
+      // (2^20: 4.47 -> 4.26 ms, 2^22: 12.9 -> 12.5 ms, profiles/r02h); smaller
+      // MSMs stay latency-optimal with the shortest chains (2^18 with 8-bucket
+      // chains: 2.53 -> 2.67 ms)
+      if (ls < 8 && (double)pl.G * pl.B >= (double)(1u << 19)) ls = 8;
     }
   }
   pl.LS = pl.B < ls ? pl.B : ls;
   pl.S = (pl.B + pl.LS - 1) / pl.LS;
 }
 
-// Window size minimising  n*W + W*B*4 + W*c*12  per task (bucket accumulation
-// vs reduction vs window-fold adds; a reduction step is ~2 full adds, ~1.4x a
-// mixed add).  nbits = scalar MODULUS_BIT_SIZE.  forced_c != 0 pins c.
+// Window size minimising  n*W + W*B*4 + W*c*12 (+ the per-block sort term
+// below) per task (bucket accumulation vs reduction vs window-fold adds; a
+// reduction step is ~2 full adds, ~1.4x a mixed add).  nbits = scalar MODULUS_BIT_SIZE.  forced_c != 0 pins c.
 static MsmPlan make_plan(size_t n, uint32_t nbits, uint32_t forced_c = 0) {
   double best = 1e300;
   MsmPlan pl{};
@@ -190,6 +197,14 @@ static MsmPlan make_plan(size_t n, uint32_t nbits, uint32_t forced_c = 0) {
     uint32_t W = (nbits + 1 + c - 1) / c;
     double B = (double)(1u << (c - 1));
     double cost = (double)n * W + W * B * 4.0 + W * c * 12.0;
+    // Window-padded keys that do not fit one 20-bit sort with the window id
+    // (msm_core_impl) are sorted block by block: each block's launch tails and
+    // its latency-bound share of the reduction cost ~0.5M mixed adds over the
+    // one-sort form (2^23: c = 16 measured 2% faster than c = 19 in
+    // profiles/r02h/c_sweep23.log; 2^24 and up keep c = 20).
+    uint32_t wbits = 0;
+    while ((1u << wbits) < W) wbits++;
+    if (n >= ((size_t)1 << 16) && c + wbits > 20) cost += W * 0.5e6;
     if (forced_c ? c == forced_c : (c >= 2 && cost < best)) {
       best = cost;
       pl.c = c;

@@ -123,6 +123,8 @@ def plan_c(n, nbits):
     for c in range(2, 23):
         w = -(-(nbits + 1) // c)
         cost = n * w + w * (1 << (c - 1)) * 4 + w * c * 12
+        if n >= 1 << 16 and c + (w - 1).bit_length() > 20:  # per-block sorts
+            cost += w * 0.5e6
         if best is None or cost < best[0]:
             best = (cost, c)
     return best[1]
