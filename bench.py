@@ -419,6 +419,8 @@ def main():
     aux = None
     if rank == 0 and world == 1 and not args.no_aux:
         aux = {}
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import coracle as co20  # checker only (KAT / inputs), never timed
         # BASELINE config 3: G1 MSM at 2^20 -- the first 2^20 resident terms, KAT-checked
         n20 = 1 << 20
         if n_loc >= n20:
@@ -428,14 +430,32 @@ def main():
                 t_a = time.perf_counter()
                 out20 = ecgpu.msm_dev(prog, args.curve, d_msm_bases, d_scal, n20)
                 best20 = min(best20, time.perf_counter() - t_a)
-            sys.path.insert(0, os.path.join(ROOT, "oracle"))
-            import coracle as co20
             k20 = co20.kat_scalar(cid, a_loc, KAT_B, scal[:n20], nthreads=nthreads) % r_int
             want20 = co20.jac_to_affine(cid, co20.gen_mul(cid, k20))
             got20 = co20.jac_to_affine(cid, out20)
             aux["msm_2p20"] = {"ms": best20 * 1e3, "point_adds_per_s": n20 / best20,
                                "kat": bool(want20 is not None and got20 is not None and (want20 == got20).all()),
                                "note": "BASELINE config 3: first 2^20 resident terms, best of 5 synchronous calls"}
+        # the reference's own multiexp bench (ag-cuda-ec/benches/multiexp.rs:15-62): 2^22 bases cycled
+        # with period 99, scalars with period 73, multiple_multiexp_st(.., 1024 chunks, window 8, false)
+        nrb = 1 << 22
+        meta_b = co20.gen_bases(cid, 41, 43, 99)
+        d_rb = ecgpu.upload_multiexp_bases(prog, np.ascontiguousarray(np.resize(meta_b, (nrb, meta_b.shape[1]))),
+                                           curve=args.curve)
+        meta_e = rand_scalars(np.random.default_rng(73), 73, r_int)
+        d_re = ecgpu.DeviceBuffer.upload(prog, np.ascontiguousarray(np.resize(meta_e, (nrb, 4))))
+        ecgpu.multiple_multiexp(prog, d_rb, (d_re, nrb), 1024, 8, False, curve=args.curve)
+        best_rb = 1e9
+        for _ in range(3):
+            t_a = time.perf_counter()
+            ecgpu.multiple_multiexp(prog, d_rb, (d_re, nrb), 1024, 8, False, curve=args.curve)
+            best_rb = min(best_rb, time.perf_counter() - t_a)
+        aux["reference_multiexp_bench_shape"] = {
+            "shape": "2^22 terms (bases period 99, scalars period 73), 1024 tasks of 4096, window 8",
+            "ms": best_rb * 1e3, "terms_per_s": nrb / best_rb,
+            "note": "the reference prints this as 'GPU took {}ms' (bases already uploaded here)"}
+        d_rb.free()
+        d_re.free()
         # batched multi-line MSM on the ag-cuda-ec AMT shape (benches/amt.rs: LOG_N=10 -> 2^21 x 10 lines)
         L, lines, chunks = 1 << 21, 10, 1 << 10
         d_lb = ecgpu.gen_bases_dev(prog, args.curve, 7, 11, L * lines)

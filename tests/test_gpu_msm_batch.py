@@ -173,3 +173,38 @@ def test_multiexp_batch_kat_large(prog, cname, cid):
         w = co.jac_to_affine(cid, co.gen_mul(cid, k))
         g = co.jac_to_affine(cid, got[t])
         assert (g is None and w is None) or (g == w).all(), t
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_multiexp_reference_bench_shape(prog, cname, cid):
+    """ag-cuda-ec/benches/multiexp.rs:15-62 as written: 2^22 bases cycled with
+    period 99, scalars cycled with period 73 (random_input_by_cycle),
+    multiple_multiexp_st(bases, exps, 1024, 8, false) -> 1024 tasks of 4096
+    terms, whose sum the bench compares with arkworks.  Here: sampled tasks
+    against multiexp_cpu and the sum of all 1024 tasks against the known answer
+    (sum_i s_(i mod 73) (a + (i mod 99) b)) G."""
+    cv = po.CURVES[cname]
+    N, CH = 1 << 22, 1024
+    clen = N // CH
+    a, b = 41, 43
+    meta_b = co.gen_bases(cid, a, b, 99)
+    bases = np.ascontiguousarray(np.resize(meta_b, (N, meta_b.shape[1])))
+    meta_e = rand_scalars(cv, 73, 73 + cid)
+    exps = np.ascontiguousarray(np.resize(meta_e, (N, 4)))
+    d_b = ecgpu.upload_multiexp_bases(prog, bases)
+    got = ecgpu.multiple_multiexp(prog, d_b, exps, CH, 8, False, curve=cname)
+    assert got.shape[0] == CH
+    for t in (0, 1, 517, CH - 1):
+        sl = slice(t * clen, (t + 1) * clen)
+        w = co.jac_to_affine(cid, co.multiexp_cpu(cid, bases[sl], exps[sl]))
+        g = co.jac_to_affine(cid, got[t])
+        assert g is not None and (g == w).all(), t
+    i = np.arange(N, dtype=np.int64)
+    cnt = np.bincount(i % 73, minlength=73)
+    m = np.zeros(73, dtype=np.int64)
+    np.add.at(m, i % 73, i % 99)
+    r = R[cname]
+    k = sum(s * (a * int(cnt[j]) + b * int(m[j])) for j, s in enumerate(co.to_ints(meta_e))) % r
+    pts = np.stack([co.jac_to_affine(cid, p) for p in got])
+    total = co.naive_multiexp(cid, pts, co.u64arr([1] * CH, 4))
+    assert (co.jac_to_affine(cid, total) == co.jac_to_affine(cid, co.gen_mul(cid, k))).all()
