@@ -90,6 +90,11 @@ static bool msm_pw_enabled() {  // A/B switch: ECG_MSM_PW=0 keeps one global sor
   static const bool v = env_u32("ECG_MSM_PW", 1) != 0;
   return v;
 }
+static bool msm_fold_rr_enabled() {  // A/B switch: ECG_MSM_FOLD_RR=0 folds batched tasks in 32-bit limbs
+  static const bool v = env_u32("ECG_MSM_FOLD_RR", 1) != 0;
+  return v;
+}
+#define ECG_MSM_FOLD_RR_ON msm_fold_rr_enabled()
 static bool msm_pw_one_enabled() {  // A/B switch: ECG_MSM_PW1=0 sorts every block on its own
   static const bool v = env_u32("ECG_MSM_PW1", 1) != 0;
   return v;
@@ -779,6 +784,25 @@ __global__ void msm_sums_to_std_kernel(const XYZZ<F>* __restrict__ in, uint32_t 
   store_xyzz(&out[i], pa_to_std(load_xyzz(&in[i])));
 }
 
+// Batched form: the per-task Horner over its W window sums in the pipeline's
+// reduced-radix point form, before the conversion (one thread per task).  The
+// fold is a latency-bound chain of c (W - 1) doublings -- 1024 tasks are 16
+// waves on 1024 SIMDs -- and the reduced-radix formulas issue their paired
+// products as independent chains where the 32-bit-limb ones wait on carries.
+template <class F>
+__global__ void __launch_bounds__(64)
+    msm_fold_rr_kernel(const XYZZ<F>* __restrict__ sums, uint32_t nw, uint32_t c, uint32_t tasks,
+                       XYZZ<F>* __restrict__ out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= tasks) return;
+  XYZZ<F> acc = load_xyzz(&sums[(size_t)t * nw + nw - 1]);
+  for (int w = (int)nw - 2; w >= 0; w--) {
+    for (uint32_t k = 0; k < c; k++) acc = pa_dbl(acc);
+    acc = pa_add(acc, load_xyzz(&sums[(size_t)t * nw + w]));
+  }
+  store_xyzz(&out[t], acc);
+}
+
 static bool msm_rr_enabled() {  // A/B switch: ECG_MSM_RR=0 runs the 32-bit-limb pipeline
   static const bool v = env_u32("ECG_MSM_RR", 1) != 0;
   return v;
@@ -909,7 +933,7 @@ static inline uint32_t blocks_for(size_t n, int threads) { return (uint32_t)((n 
 // (msm_prepare_t), so the per-call conversion is skipped.
 template <class C, class AF>
 int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
-                  const MsmPlan& pl0, hipStream_t s, void** d_sums, bool prepared) {
+                  const MsmPlan& pl0, hipStream_t s, void** d_sums, bool prepared, bool* folded) {
   using F = AF;
   using X = XYZZ<F>;
   MsmPlan pl = pl0;  // reduction segments sized for this point form's occupancy
@@ -1056,10 +1080,20 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   if constexpr (std::is_same<F, typename C::Fq>::value) {
     *d_sums = in;
   } else {  // window sums back to the 32-bit-limb form (canonical coordinates)
+    uint32_t npts = pl.G;
+    if (folded && pl.fold_windows() > 1 && ECG_MSM_FOLD_RR_ON) {  // batched: Horner per task first
+      const uint32_t tasks = pl.G / pl.W;
+      hipLaunchKernelGGL(msm_fold_rr_kernel<F>, dim3(blocks_for(tasks, 64)), dim3(64), 0, s, (const X*)in, pl.W,
+                         pl.c, tasks, out);
+      ECG_HIP(hipGetLastError());
+      in = out;
+      npts = tasks;
+      *folded = true;
+    }
     void* st;
     ECG_TRY(ws_get(ctx, "msm_sums_std", (size_t)pl.G * sizeof(XYZZ<typename C::Fq>), &st));
-    hipLaunchKernelGGL((msm_sums_to_std_kernel<F, typename C::Fq>), dim3(blocks_for(pl.G, 64)), dim3(64), 0, s,
-                       (const X*)in, pl.G, (XYZZ<typename C::Fq>*)st);
+    hipLaunchKernelGGL((msm_sums_to_std_kernel<F, typename C::Fq>), dim3(blocks_for(npts, 64)), dim3(64), 0, s,
+                       (const X*)in, npts, (XYZZ<typename C::Fq>*)st);
     ECG_HIP(hipGetLastError());
     *d_sums = st;
   }
@@ -1067,14 +1101,19 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
 }
 
 // Steps 1-6; leaves pl.G window sums (lazy 32-bit-limb XYZZ) on the device.
+// folded != nullptr (batched form): the reduced-radix pipeline may fold each
+// task's windows itself (Horner, msm_fold_rr_kernel) and then leaves one sum
+// per task and sets *folded.
 template <class C>
 int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g, const MsmPlan& pl,
-               hipStream_t s, void** d_sums, bool prepared = false) {
+               hipStream_t s, void** d_sums, bool prepared = false, bool* folded = nullptr) {
+  if (folded) *folded = false;
   if constexpr (MsmField<C>::rr) {
     if (msm_rr_enabled())
-      return msm_core_impl<C, typename MsmField<C>::type>(ctx, d_bases, d_scalars, g, pl, s, d_sums, prepared);
+      return msm_core_impl<C, typename MsmField<C>::type>(ctx, d_bases, d_scalars, g, pl, s, d_sums, prepared,
+                                                          folded);
   }
-  return msm_core_impl<C, typename C::Fq>(ctx, d_bases, d_scalars, g, pl, s, d_sums, prepared);
+  return msm_core_impl<C, typename C::Fq>(ctx, d_bases, d_scalars, g, pl, s, d_sums, prepared, nullptr);
 }
 
 // Bytes per base in the pipeline's own layout: 128-B reduced-radix records
@@ -1468,9 +1507,12 @@ int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const 
     return ECG_ERR_INVALID;
   }
   void *d_sums, *d_out;
-  ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums, prepared));
+  bool folded = false;
+  ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums, prepared, &folded));
   ECG_TRY(ws_get(ctx, "msm_batch_out", ob, &d_out));
-  hipLaunchKernelGGL(msm_fold_kernel<C>, dim3(blocks_for(tasks, 64)), dim3(64), 0, s, (const XYZZ<F>*)d_sums, pl,
+  MsmPlan pf = pl;
+  if (folded) pf.tab = 1;  // one (already folded) sum per task: normalisation only
+  hipLaunchKernelGGL(msm_fold_kernel<C>, dim3(blocks_for(tasks, 64)), dim3(64), 0, s, (const XYZZ<F>*)d_sums, pf,
                      tasks, (F*)d_out);
   ECG_HIP(hipGetLastError());
   ECG_HIP(hipMemcpyAsync(out_jac, d_out, ob, hipMemcpyDeviceToHost, s));
