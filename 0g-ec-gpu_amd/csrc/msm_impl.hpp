@@ -1480,6 +1480,10 @@ int msm_host_t(ecg_ctx* ctx, const void* h_bases, const void* h_scalars, size_t 
 // pass -- one sort over (task, window, bucket) keys, one accumulation launch,
 // one reduction -- then a device fold per task.  out_jac: tasks x 3 x Fq,
 // line-major (results[line * n_chunks + chunk], multiexp.cl:260).
+// Batched results normalised on the host (one batch inversion) up to this many
+// tasks; more tasks keep the device's thread-per-task normalisation, whose
+// latency does not grow with the task count.
+constexpr uint32_t MSM_HOST_NORM_TASKS = 2048;
 template <class C>
 int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
                        uint32_t window_bits, uint64_t* out_jac, hipStream_t s, BaseForm bf) {
@@ -1510,6 +1514,51 @@ int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const 
   bool folded = false;
   ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums, prepared, &folded));
   ECG_TRY(ws_get(ctx, "msm_batch_out", ob, &d_out));
+  if (folded && tasks <= MSM_HOST_NORM_TASKS) {
+    // normalisation on the host with one inversion for all tasks (Montgomery's
+    // trick): a device thread per task would wait out a ~380-squaring Fermat
+    // chain of its own
+    using HF = HostF<C>;
+    using HX = host::HPoint<HF>;
+    std::vector<XYZZ<F>> sums(tasks);
+    ECG_HIP(hipMemcpyAsync(sums.data(), d_sums, (size_t)tasks * sizeof(XYZZ<F>), hipMemcpyDeviceToHost, s));
+    ECG_HIP(hipStreamSynchronize(s));
+    std::vector<HX> pts(tasks);
+    std::vector<HF> pre(tasks);
+    HF run = HF::one();
+    for (uint32_t t = 0; t < tasks; t++) {
+      static_assert(sizeof(pts[t].X) == sizeof(sums[t].X), "host/device coordinate layouts differ");
+      memcpy(&pts[t].X, &sums[t].X, sizeof(pts[t].X));
+      memcpy(&pts[t].Y, &sums[t].Y, sizeof(pts[t].Y));
+      memcpy(&pts[t].ZZ, &sums[t].ZZ, sizeof(pts[t].ZZ));
+      memcpy(&pts[t].ZZZ, &sums[t].ZZZ, sizeof(pts[t].ZZZ));
+      pts[t].X = host::hcanon(pts[t].X);  // device values are in the lazy range [0, 2p]
+      pts[t].Y = host::hcanon(pts[t].Y);
+      pts[t].ZZ = host::hcanon(pts[t].ZZ);
+      pts[t].ZZZ = host::hcanon(pts[t].ZZZ);
+      pre[t] = run;  // product of the (ZZ ZZZ) of the non-identity points before t
+      if (!pts[t].is_zero()) run = host::hmul(run, host::hmul(pts[t].ZZ, pts[t].ZZZ));
+    }
+    HF inv = host::hinv(run);  // 1 / prod (ZZ ZZZ)
+    constexpr int N = HF::N;
+    for (int t = (int)tasks - 1; t >= 0; t--) {
+      uint64_t* o = out_jac + (size_t)t * 3 * N;
+      if (pts[t].is_zero()) {
+        host::hto_jac_norm(pts[t], o);
+        continue;
+      }
+      const HF d = host::hmul(pts[t].ZZ, pts[t].ZZZ);
+      const HF it = host::hmul(inv, pre[t]);  // 1 / (ZZ ZZZ) of point t
+      inv = host::hmul(inv, d);
+      const HF x = host::hmul(pts[t].X, host::hmul(it, pts[t].ZZZ));
+      const HF y = host::hmul(pts[t].Y, host::hmul(it, pts[t].ZZ));
+      const HF one = HF::one();
+      memcpy(o, &x, 8 * N);
+      memcpy(o + N, &y, 8 * N);
+      memcpy(o + 2 * N, &one, 8 * N);
+    }
+    return ECG_OK;
+  }
   MsmPlan pf = pl;
   if (folded) pf.tab = 1;  // one (already folded) sum per task: normalisation only
   hipLaunchKernelGGL(msm_fold_kernel<C>, dim3(blocks_for(tasks, 64)), dim3(64), 0, s, (const XYZZ<F>*)d_sums, pf,

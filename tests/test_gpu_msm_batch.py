@@ -208,3 +208,27 @@ def test_multiexp_reference_bench_shape(prog, cname, cid):
     pts = np.stack([co.jac_to_affine(cid, p) for p in got])
     total = co.naive_multiexp(cid, pts, co.u64arr([1] * CH, 4))
     assert (co.jac_to_affine(cid, total) == co.jac_to_affine(cid, co.gen_mul(cid, k))).all()
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_multiexp_batch_many_tasks(prog, cname, cid):
+    """More tasks than the host normalises in one batch inversion (> 2048:
+    3 lines x 1024 chunks of 8 terms), so the device's per-task normalisation
+    runs; every 97th task and the last against multiexp_cpu, plus an identity
+    task (all-zero scalars in one chunk)."""
+    cv = po.CURVES[cname]
+    LINES, L, CH = 3, 1 << 13, 1024
+    clen = L // CH
+    bases = co.gen_bases(cid, 5, 7, LINES * L)
+    exps = rand_scalars(cv, L, 99 + cid)
+    exps[3 * clen:4 * clen] = 0
+    d_b = ecgpu.upload_multiexp_bases(prog, bases)
+    got = ecgpu.multiple_multiexp(prog, d_b, exps, CH, 0, True, curve=cname)
+    assert got.shape[0] == LINES * CH
+    for t in list(range(0, LINES * CH, 97)) + [3, CH + 3, LINES * CH - 1]:
+        l, c = divmod(t, CH)
+        b = bases[l * L + c * clen: l * L + (c + 1) * clen]
+        e = exps[c * clen: (c + 1) * clen]
+        w = co.jac_to_affine(cid, co.multiexp_cpu(cid, b, e))
+        g = co.jac_to_affine(cid, got[t])
+        assert (g is None and w is None) or (g is not None and w is not None and (g == w).all()), t
