@@ -8,8 +8,9 @@
 //   * MSM: ncclAllGather of the per-rank Jacobian partial (3 x Lq u64),
 //     then the EC fold (RCCL has no EC-add reduction);
 //   * one NTT split over ranks: three equal-split ncclAllToAll (dfft.hip).
-// Rendezvous (the 128-byte ncclUniqueId) travels through the caller's
-// launcher (torch.distributed over gloo in bench.py / ecgpu.dist).
+// Rendezvous: the 128-byte ncclUniqueId travels through the caller's
+// launcher (ecgpu.dist.HostGroup in bench.py: one authenticated local socket
+// per rank, no torch in the process).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 

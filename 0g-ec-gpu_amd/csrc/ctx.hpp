@@ -83,14 +83,9 @@ struct ecg_ctx {
     uint64_t fingerprint = 0;  // sampled host records at upload time
   };
   std::vector<BaseCache> base_cache;
-  // bases held in the bucket kernels' own layout (ecg_msm_prepare_bases,
-  // upload_multiexp_bases's role): prepared device pointer -> (curve, count)
-  struct Prepared {
-    int curve = -1;
-    size_t n = 0;
-    uint32_t tab_c = 0;  // > 0: window table of window size tab_c (ecg_msm_prepare_table)
-  };
-  std::map<const void*, Prepared> prepared;
+  // (prepared bases -- ecg_msm_prepare_bases -- live in a process-wide
+  // registry keyed by device and address range, msm.hip, so any context on
+  // the device and any base-aligned pointer into them are recognised)
   // MSM terms per device pass (SingleMultiexpKernel::n, multiexp.rs:71-93);
   // 0 = derived from device memory (msm_chunk_terms)
   size_t msm_chunk = 0;
@@ -150,7 +145,7 @@ int comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes_p
 void comm_free(ecg_ctx* ctx);
 int comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes, hipStream_t s);
 // Bases [x, y] -> a new device buffer in the bucket kernels' layout,
-// registered in ctx->prepared (ecg_msm_prepare_bases).
+// registered in the process-wide prepared-bases registry (msm.hip).
 // How the bucket kernels read d_bases: the boundary [x, y] layout, prepared
 // records (ecg_msm_prepare_bases), or a window table (ecg_msm_prepare_table):
 // tab_c > 0, record i W + k = 2^(k tab_c) P_i for the tab_n bases, k < W.
@@ -163,6 +158,14 @@ struct BaseForm {
 // tab_c > 0: also the window table (rows 2^(k tab_c) P, ecg_msm_prepare_table).
 int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, uint32_t tab_c, void** d_out,
                     hipStream_t s);
+// Release a prepared buffer (its header allocation) if p is one: true when
+// handled, false for any other pointer (the caller frees it).
+bool msm_prepared_free(void* p);
+size_t msm_prepared_stride(int curve_id, uint32_t tab_c);  // bytes per base of a prepared buffer
+// Plan of a one-task MSM of n terms (window_bits = 0: automatic): window
+// bits, windows, and how the sorted entries are grouped (ECG_SORT_* in ecgpu.h).
+int msm_plan_info_run(int curve_id, size_t n, uint32_t window_bits, uint32_t* c, uint32_t* windows,
+                      int* sort_mode);
 // Window size of an automatic window table for n-term MSMs.
 uint32_t msm_table_window_auto(int curve_id, size_t n);
 int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_bases, const void* d_scalars,

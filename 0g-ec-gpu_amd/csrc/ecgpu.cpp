@@ -441,6 +441,10 @@ int ecg_msm_prepare_bases(ecg_ctx* ctx, int curve_id, const void* d_bases, size_
   return msm_prepare_run(ctx, curve_id, d_bases, n, 0, d_prepared, ctx->stream);
 }
 
+size_t ecg_msm_prepared_stride(int curve_id, uint32_t window_bits) {
+  return curve_valid(curve_id) ? msm_prepared_stride(curve_id, window_bits) : 0;
+}
+
 uint32_t ecg_msm_table_window(int curve_id, size_t n) {
   if (!curve_valid(curve_id)) return 0;
   return msm_table_window_auto(curve_id, n);
@@ -497,9 +501,27 @@ static void base_cache_free(ecg_ctx* ctx) {
 
 void ecg_base_cache_clear(ecg_ctx* ctx) {
   if (!ctx) return;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   base_cache_free(ctx);
+}
+
+size_t ecg_base_cache_keys(ecg_ctx* ctx, const void** out, size_t cap) {
+  if (!ctx) return 0;
+  std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+  const size_t n = ctx->base_cache.size();
+  for (size_t k = 0; k < n && k < cap && out; k++) out[k] = ctx->base_cache[k].host;
+  return n;
+}
+
+int ecg_msm_plan_info(int curve_id, size_t n, uint32_t window_bits, uint32_t* c, uint32_t* windows,
+                      int* sort_mode) {
+  if (!c || !windows || !sort_mode) {
+    set_error("ecg_msm_plan_info: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  return msm_plan_info_run(curve_id, n, window_bits, c, windows, sort_mode);
 }
 
 // FNV-1a over up to 16 evenly spaced host records (first and last included):
@@ -663,8 +685,8 @@ void ecg_dev_free(ecg_ctx* ctx, void* p) {
   std::lock_guard<std::recursive_mutex> lk(ctx->mu);
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
-  ctx->prepared.erase(p);  // a prepared-bases buffer is unregistered with its memory
-  (void)hipFree(p);
+  // a prepared-bases buffer (from any context) is unregistered with its memory
+  if (!msm_prepared_free(p)) (void)hipFree(p);
 }
 
 int ecg_dev_upload(ecg_ctx* ctx, void* d_dst, const void* src, size_t bytes) {
@@ -698,6 +720,17 @@ int ecg_msm_multi(ecg_ctx** ctxs, int nctx, int curve_id, const uint64_t* bases_
   std::mutex mu;
   std::string err_msg;
   std::vector<std::thread> th;
+  // every worker polls this before each device pass: the caller's abort, or
+  // another worker's error (first error wins, multiexp.rs:354-359)
+  struct Poll {
+    ecg_abort_cb cb;
+    void* user;
+    std::atomic<int>* first_err;
+    static int fn(void* p) {
+      const Poll* q = (const Poll*)p;
+      return q->first_err->load() != ECG_OK || (q->cb && q->cb(q->user)) ? 1 : 0;
+    }
+  } poll{abort_cb, user, &first_err};
   int used = 0;
   for (int d = 0; d < nctx; d++) {
     const size_t i0 = std::min(n, d * chunk), i1 = std::min(n, i0 + chunk);
@@ -705,7 +738,7 @@ int ecg_msm_multi(ecg_ctx** ctxs, int nctx, int curve_id, const uint64_t* bases_
     used++;
     th.emplace_back([&, d, i0, i1]() {
       int rc = msm_host(ctxs[d], curve_id, bases_xy + i0 * 2 * lq, scalars + i0 * 4, i1 - i0,
-                        partials.data() + (size_t)d * 3 * lq, abort_cb, user);
+                        partials.data() + (size_t)d * 3 * lq, &Poll::fn, &poll);
       if (rc != ECG_OK) {
         int expected = ECG_OK;
         if (first_err.compare_exchange_strong(expected, rc)) {

@@ -1,6 +1,9 @@
 // curve_id dispatch of the MSM drivers.  The per-curve kernels and drivers
 // (msm_impl.hpp) are compiled once per curve in msm_inst.hip (-DECG_INST=id),
 // which exports one MsmOps table each; this file only routes calls.
+#include <atomic>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "ctx.hpp"
@@ -22,22 +25,110 @@ static const MsmOps* msm_ops(int curve_id, const char* what) {
   }
 }
 
-// Is d_bases a prepared buffer (ecg_msm_prepare_bases / _table)?  It must
-// then cover the n bases the call reads, for the same curve.
+// ---------------------------------------------------------------------------
+// Prepared-bases registry (ecg_msm_prepare_bases / _table).  Process-wide,
+// keyed by the data's address range, so a prepared buffer is recognised from
+// any context on its device and through any base-aligned pointer into it
+// (e.g. one rank's shard handed to ecg_msm_dist).  Each allocation starts
+// with a header (magic + a per-buffer nonce) in front of the records: a
+// buffer released behind the library's back (hipFree of some other pointer
+// cannot be seen) and reused by a new allocation no longer carries its
+// nonce, so a stale entry is detected and dropped instead of its memory
+// being read as records.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr size_t PREP_HEADER = 256;  // keeps the records 256-B aligned
+constexpr uint64_t PREP_MAGIC = 0x3150455250474345ull;  // "ECGPREP1"
+struct PrepEntry {
+  int device;
+  int curve;
+  size_t n;         // bases
+  uint32_t tab_c;   // > 0: window table (ecg_msm_prepare_table)
+  size_t stride;    // bytes per base (all of its table rows)
+  uint64_t nonce;
+};
+std::mutex g_prep_mu;
+std::map<uintptr_t, PrepEntry> g_prep;  // records' start address -> entry
+std::atomic<uint64_t> g_prep_seq{0x9E3779B97F4A7C15ull};
+}  // namespace
+
+// Is d_bases inside a prepared buffer?  It must then sit on a base boundary,
+// on ctx's device, and cover the n bases the call reads, for the same curve.
 static int prepared_lookup(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, const char* what,
                            BaseForm* bf) {
   *bf = BaseForm{};
-  auto it = ctx->prepared.find(d_bases);
-  if (it == ctx->prepared.end()) return ECG_OK;
-  if (it->second.curve != curve_id || n > it->second.n) {
-    set_error("%s: prepared bases are %zu bases of curve %d, the call reads %zu of curve %d", what, it->second.n,
-              it->second.curve, n, curve_id);
+  const uintptr_t a = (uintptr_t)d_bases;
+  PrepEntry e;
+  uintptr_t start;
+  {
+    std::lock_guard<std::mutex> g(g_prep_mu);
+    auto it = g_prep.upper_bound(a);
+    if (it == g_prep.begin()) return ECG_OK;
+    --it;
+    if (a >= it->first + it->second.n * it->second.stride && !(it->second.n == 0 && a == it->first)) return ECG_OK;
+    start = it->first;
+    e = it->second;
+  }
+  // still our allocation?  (header written at prepare time)
+  uint64_t hdr[2] = {0, 0};
+  if (hipMemcpy(hdr, (const void*)(start - PREP_HEADER), sizeof hdr, hipMemcpyDeviceToHost) != hipSuccess ||
+      hdr[0] != PREP_MAGIC || hdr[1] != e.nonce) {
+    (void)hipGetLastError();
+    std::lock_guard<std::mutex> g(g_prep_mu);
+    auto it = g_prep.find(start);
+    if (it != g_prep.end() && it->second.nonce == e.nonce) g_prep.erase(it);  // freed outside the library
+    return ECG_OK;
+  }
+  if (e.device != ctx->device) {
+    set_error("%s: the prepared bases live on device %d, the context is on device %d", what, e.device, ctx->device);
+    return ECG_ERR_INVALID;
+  }
+  const size_t off = a - start;
+  if (off % e.stride) {
+    set_error("%s: pointer %zu bytes into prepared bases is not on a base boundary (%zu bytes per base)", what, off,
+              e.stride);
+    return ECG_ERR_INVALID;
+  }
+  const size_t avail = e.n - off / e.stride;
+  if (e.curve != curve_id || n > avail) {
+    set_error("%s: prepared bases hold %zu bases of curve %d from this pointer, the call reads %zu of curve %d", what,
+              avail, e.curve, n, curve_id);
     return ECG_ERR_INVALID;
   }
   bf->prepared = true;
-  bf->tab_c = it->second.tab_c;
-  bf->tab_n = it->second.n;
+  bf->tab_c = e.tab_c;
+  bf->tab_n = avail;
   return ECG_OK;
+}
+
+bool msm_prepared_free(void* p) {
+  std::lock_guard<std::mutex> g(g_prep_mu);
+  auto it = g_prep.find((uintptr_t)p);
+  if (it == g_prep.end()) return false;
+  const uint64_t zero[2] = {0, 0};  // retire the header: a later lookup of a reused address cannot match
+  (void)hipMemcpy((char*)p - PREP_HEADER, zero, sizeof zero, hipMemcpyHostToDevice);
+  (void)hipFree((char*)p - PREP_HEADER);
+  (void)hipGetLastError();
+  g_prep.erase(it);
+  return true;
+}
+
+size_t msm_prepared_stride(int curve_id, uint32_t tab_c) {
+  const MsmOps* o = msm_ops(curve_id, "prepared_stride");
+  if (!o) return 0;
+  if (!tab_c) return o->record_bytes();
+  const uint32_t W = tab_c >= 2 && tab_c <= 25 ? o->table_windows(tab_c) : 0u;
+  return W ? o->record_bytes() * W : 0;
+}
+
+int msm_plan_info_run(int curve_id, size_t n, uint32_t window_bits, uint32_t* c, uint32_t* windows, int* sort_mode) {
+  const MsmOps* o = msm_ops(curve_id, "plan_info");
+  if (!o) return ECG_ERR_INVALID;
+  if (window_bits > 22) {
+    set_error("plan_info: window_bits %u out of range [0, 22] (0 = automatic)", window_bits);
+    return ECG_ERR_INVALID;
+  }
+  return o->plan_info(n, window_bits, c, windows, sort_mode);
 }
 
 int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, uint64_t* out_jac,
@@ -78,23 +169,31 @@ int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, u
     }
   }
   const size_t bytes = o->prepared_bytes(n, tab_c);
-  void* p = nullptr;
-  hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
+  void* base = nullptr;
+  hipError_t e = hipMalloc(&base, bytes + PREP_HEADER);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     set_error("prepare_bases: device allocation of %zu bytes failed: %s", bytes, hipGetErrorString(e));
     return ECG_ERR_NOMEM;
   }
+  void* p = (char*)base + PREP_HEADER;
+  const uint64_t nonce = g_prep_seq.fetch_add(0x9E3779B97F4A7C15ull) ^ (uint64_t)(uintptr_t)p;
+  const uint64_t hdr[2] = {PREP_MAGIC, nonce};
   int rc = o->prepare(ctx, d_bases, n, tab_c, p, s);
-  if (rc == ECG_OK && hipStreamSynchronize(s) != hipSuccess) {
+  if (rc == ECG_OK && (hipMemcpyAsync(base, hdr, sizeof hdr, hipMemcpyHostToDevice, s) != hipSuccess ||
+                       hipStreamSynchronize(s) != hipSuccess)) {
     set_error("prepare_bases: %s", hipGetErrorString(hipGetLastError()));
     rc = ECG_ERR_HIP;
   }
   if (rc != ECG_OK) {
-    (void)hipFree(p);
+    (void)hipFree(base);
     return rc;
   }
-  ctx->prepared[p] = {curve_id, n, tab_c};
+  const size_t stride = o->record_bytes() * (tab_c ? o->table_windows(tab_c) : 1u);
+  {
+    std::lock_guard<std::mutex> g(g_prep_mu);
+    g_prep[(uintptr_t)p] = PrepEntry{ctx->device, curve_id, n, tab_c, stride, nonce};
+  }
   *d_out = p;
   return ECG_OK;
 }

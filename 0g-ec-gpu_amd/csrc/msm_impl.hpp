@@ -925,6 +925,36 @@ __global__ void __launch_bounds__(64)
 // ---------------------------------------------------------------------------
 static inline uint32_t blocks_for(size_t n, int threads) { return (uint32_t)((n + threads - 1) / threads); }
 
+// How the (key, value) entries of one pass are sorted (ECG_SORT_* in ecgpu.h):
+//  * GLOBAL:   global keys (group * B + bucket), one sort over every entry --
+//              batched tasks, window tables, and passes below 2^16 terms;
+//  * PW_ONE:   window-padded keys whose window id and bucket fit 20 bits
+//              together (c + log2 W <= 20, i.e. c <= 16 up to 2^22 terms):
+//              ONE 2-pass sort over all blocks;
+//  * PW_BLOCK: window-padded keys, one 2-pass sort over the c-bit key per
+//              window block (c = 20 from 2^24 terms: the headline plan).
+// m = scalars of the row, line_groups = n_chunks * W.
+static int msm_sort_mode(const MsmPlan& pl, size_t m, uint32_t n_chunks, uint32_t line_groups) {
+  const bool pw = msm_pw_enabled() && !pl.tab && n_chunks == 1 && m >= ((size_t)1 << 16) &&
+                  ((uint64_t)line_groups << pl.c) < 0xffffffffull;
+  if (!pw) return ECG_SORT_GLOBAL;
+  uint32_t wbits = 0;
+  while ((1u << wbits) < line_groups) wbits++;
+  return msm_pw_one_enabled() && pl.c + wbits <= 20 ? ECG_SORT_PW_ONE : ECG_SORT_PW_BLOCK;
+}
+
+// The plan a one-task MSM of n terms runs (ecg_msm_plan_info): the single
+// MSM (window_bits = 0) or multiple_multiexp with one chunk and the window
+// pinned to window_bits.
+template <class C>
+int msm_plan_info_t(size_t n, uint32_t window_bits, uint32_t* c, uint32_t* windows, int* sort_mode) {
+  const MsmPlan pl = make_plan(n, (uint32_t)C::FrParams::BITS, window_bits);
+  *c = pl.c;
+  *windows = pl.W;
+  *sort_mode = msm_sort_mode(pl, n, 1, pl.W);
+  return ECG_OK;
+}
+
 // Steps 1-6 for one device pass: leaves pl.G window sums (lazy XYZZ) on the
 // device and returns their address in *d_sums.
 // AF = coordinate field of the bucket pipeline (C::Fq, or FpR<Q> for the
@@ -941,13 +971,13 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   const size_t m = (size_t)g.n_chunks * g.clen;  // scalars consumed
   const uint32_t nb = pl.G * pl.B;
   const uint32_t sentinel = nb;
-  // window-padded keys (KeyMap) when every (window, line) block is one group
-  // and large enough for a sort of its own
-  const bool pw = msm_pw_enabled() && !pl.tab && g.n_chunks == 1 && m >= ((size_t)1 << 16) &&
-                  ((uint64_t)(pl.G / g.n_lines) << pl.c) < 0xffffffffull;
-  const size_t mpad = pw ? (m + pl.seg - 1) / pl.seg * pl.seg : m;
   // one line's entries (every line shares the scalar row; see msm_digits_kernel)
   const uint32_t line_groups = pl.G / g.n_lines;  // n_chunks * W
+  // window-padded keys (KeyMap) when every (window, line) block is one group
+  // and large enough for a sort of its own
+  const int sort_mode = msm_sort_mode(pl, m, g.n_chunks, line_groups);
+  const bool pw = sort_mode != ECG_SORT_GLOBAL;
+  const size_t mpad = pw ? (m + pl.seg - 1) / pl.seg * pl.seg : m;
   const size_t total = (size_t)pl.W * mpad;
   const KeyMap km{pw ? pl.c : 0u, pl.B, line_groups * pl.B};
   int key_bits = 1;
@@ -1003,7 +1033,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   // at 2^20: 2.7 of the 7.1 ms MSM) or onesweep launch tails.
   uint32_t wbits = 0;
   while ((1u << wbits) < line_groups) wbits++;
-  const bool pw_one = pw && msm_pw_one_enabled() && pl.c + wbits <= 20;
+  const bool pw_one = sort_mode == ECG_SORT_PW_ONE;
   const int cfg = pw ? msm_sort_cfg() : 0;
   const size_t sort_n = pw && !pw_one ? mpad : total;  // one sort per block, or one sort of all blocks
   const int sort_bits = pw ? (int)(pw_one ? pl.c + wbits : pl.c) : key_bits;

@@ -21,6 +21,8 @@ struct MsmOps {
   size_t (*pass_terms)(const ecg_ctx*);
   int (*host)(ecg_ctx*, const void* h_bases, const void* h_scalars, size_t n, uint64_t* out_jac, ecg_abort_cb,
               void* user);
+  size_t (*record_bytes)();  // bytes per prepared base record (one table row)
+  int (*plan_info)(size_t n, uint32_t window_bits, uint32_t* c, uint32_t* windows, int* sort_mode);
 };
 
 }  // namespace ecg

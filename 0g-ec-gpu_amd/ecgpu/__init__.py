@@ -106,6 +106,11 @@ _SIGS = {
                                   ctypes.c_size_t, _u64p, ctypes.c_int, ctypes.c_size_t, _u64p, ctypes.c_int, _u64p,
                                   ABORT_CB, ctypes.c_void_p]),
     "ecg_base_cache_clear": (None, [ctypes.c_void_p]),
+    "ecg_base_cache_keys": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]),
+    "ecg_msm_plan_info": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.c_uint32,
+                                         ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                         ctypes.POINTER(ctypes.c_int)]),
+    "ecg_msm_prepared_stride": (ctypes.c_size_t, [ctypes.c_int, ctypes.c_uint32]),
     "ecg_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "ecg_msm_chunk_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "ecg_ctx_set_msm_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
@@ -400,6 +405,42 @@ class PreparedBases(DeviceBuffer):
 
     def read(self, dtype=np.uint64, shape=None) -> np.ndarray:
         raise EcError("PreparedBases hold the kernels' internal layout")
+
+    def stride(self) -> int:
+        """Bytes per base (all of its window-table rows)."""
+        wt = self.window_table if self.window_table > 0 else 0
+        if self.window_table < 0:
+            raise EcError("PreparedBases.stride: automatic window table (pass the window size to prepare_bases)")
+        return int(lib().ecg_msm_prepared_stride(self.curve_id, wt))
+
+    def view(self, start: int, count: int | None = None) -> "PreparedView":
+        """Bases start.. of this buffer in the same form (a base-aligned
+        pointer into it, e.g. one rank's shard); no copy.  The view borrows
+        this buffer: keep it alive while the view is used."""
+        count = self.n - start if count is None else count
+        if not (0 <= start and 0 <= count and start + count <= self.n):
+            raise EcError(f"PreparedBases.view: [{start}, {start + count}) outside [0, {self.n})")
+        return PreparedView(self, start, count)
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().ecg_dev_free(self.program.handle, self.ptr)
+            self.ptr = None
+
+
+class PreparedView(PreparedBases):
+    """Base-aligned slice of PreparedBases (does not own memory)."""
+
+    def __init__(self, parent: PreparedBases, start: int, count: int):
+        self._parent = parent
+        super().__init__(parent.program, ctypes.c_void_p(parent.ptr.value + start * parent.stride()),
+                         parent.curve_id, count, parent.window_table)
+
+    def free(self) -> None:  # the parent owns the allocation
+        self.ptr = None
+
+    def __del__(self):
+        pass
 
 
 def prepare_bases(prog: Program, curve, d_bases: DeviceBuffer, n: int, window_table=None) -> PreparedBases:
@@ -864,7 +905,7 @@ class MultiexpKernel:
                 raise EcError("multiexp_ex(cache_bases=True) needs a C-contiguous uint64 bases array "
                               "(a converted copy cannot be cached by address)")
             pins = k.program.__dict__.setdefault("_base_pins", {})
-            pins[b.ctypes.data] = bases
+            pins[b.ctypes.data] = bases  # keeps the cached array alive (the cache holds its address)
         e = np.ascontiguousarray(exps, dtype=np.uint64).reshape(-1, 4)
         dens = None
         if density is not None and not isinstance(density, FullDensity):
@@ -876,6 +917,8 @@ class MultiexpKernel:
                                   b.shape[0], skip, _ptr(e), int(exps_montgomery), e.shape[0],
                                   _ptr(dens) if dens is not None else None, int(cache_bases), _ptr(out), cb, None)
         del keep
+        if "_base_pins" in k.program.__dict__:
+            _prune_base_pins(k.program)
         _check(rc, "multiexp")
         return out
 
@@ -883,6 +926,30 @@ class MultiexpKernel:
         for k in self.kernels:
             lib().ecg_base_cache_clear(k.program.handle)
             k.program.__dict__.pop("_base_pins", None)
+
+
+def _prune_base_pins(prog: Program) -> None:
+    """Drop the references to host arrays the C base cache no longer holds
+    (evicted as the oldest of its 8 entries, or replaced after a content
+    change at the same address), so they are not kept alive for the life of
+    the Program."""
+    cap = 64
+    keys = (ctypes.c_void_p * cap)()
+    n = lib().ecg_base_cache_keys(prog.handle, keys, cap)
+    live = {keys[i] for i in range(min(n, cap))}
+    pins = prog.__dict__.get("_base_pins", {})
+    for addr in [a for a in pins if a not in live]:
+        del pins[addr]
+
+
+def msm_plan(curve, n: int, window_bits: int = 0) -> tuple[int, int, str]:
+    """(c, windows, sort) of a one-task MSM of n terms (ecg_msm_plan_info):
+    sort is "global", "pw_one" (one sort over every window block) or
+    "pw_block" (one sort per window block)."""
+    c, w, mode = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_int()
+    _check(lib().ecg_msm_plan_info(_curve(curve), int(n), int(window_bits), ctypes.byref(c), ctypes.byref(w),
+                                   ctypes.byref(mode)), "msm_plan")
+    return c.value, w.value, {0: "global", 1: "pw_one", 2: "pw_block"}[mode.value]
 
 
 def check_bases(curve, bases: np.ndarray, exps: np.ndarray) -> None:

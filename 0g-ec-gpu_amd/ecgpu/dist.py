@@ -27,6 +27,8 @@ exercise the same split.
 """
 from __future__ import annotations
 
+import hashlib
+import json
 import os
 import time
 from typing import Any, Callable, Sequence
@@ -34,62 +36,132 @@ from typing import Any, Callable, Sequence
 
 class HostGroup:
     """Rank 0 listens on (addr, port); every other rank connects.  Collectives
-    are star-shaped through rank 0 (small host objects only: ids, timings,
-    digests).  From a torch.distributed.run launch: HostGroup.from_env()."""
+    are star-shaped through rank 0 (small host values only: the RCCL id,
+    timings, digests).  From a torch.distributed.run launch: HostGroup.from_env().
+
+    Wire format: length-prefixed JSON frames (None / bool / int / float / str /
+    bytes / lists / str-keyed dicts) -- nothing received is ever unpickled or
+    executed.  A peer joins by answering rank 0's random challenge with
+    HMAC-SHA256(key, challenge || rank); the key is ECGPU_HOSTGROUP_KEY if set,
+    else derived from the launch (TORCHELASTIC_RUN_ID and MASTER_PORT, which
+    every rank of one launch shares).  Rank 0 drops connections that fail the
+    handshake, name an out-of-range or duplicate rank, or stall, and keeps
+    accepting until every rank has joined or `timeout` expires."""
+
+    _MAX_FRAME = 1 << 20
 
     def __init__(self, rank: int, world: int, addr: str = "127.0.0.1", port: int = 29600,
-                 authkey: bytes = b"ecgpu-hostgroup", timeout: float = 300.0):
-        from multiprocessing.connection import Client, Listener
+                 key: bytes | None = None, timeout: float = 300.0, bind_addr: str | None = None):
+        import socket
 
         if world <= 0 or not (0 <= rank < world):
             raise ValueError("bad world/rank")
         self.rank, self.world = rank, world
-        self._peers = []
+        self._peers: list = []
         self._conn = None
         self._listener = None
+        self._timeout = timeout
         if world == 1:
             return
+        self._key = key if key is not None else _launch_key(port)
+        deadline = time.time() + timeout
         if rank == 0:
-            self._listener = Listener((addr, port), authkey=authkey)
-            peers = {}
+            ls = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            ls.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            ls.bind((bind_addr or addr, port))
+            ls.listen(world)
+            self._listener = ls
+            peers: dict = {}
             while len(peers) < world - 1:
-                c = self._listener.accept()
-                r = c.recv()
+                left = deadline - time.time()
+                if left <= 0:
+                    self.close()
+                    raise TimeoutError(f"HostGroup: {len(peers) + 1} of {world} ranks joined within {timeout} s")
+                ls.settimeout(left)
+                try:
+                    c, _ = ls.accept()
+                except socket.timeout:
+                    continue
+                r = self._admit(c, peers)
+                if r is None:
+                    c.close()
+                    continue
                 peers[r] = c
             self._peers = [peers[r] for r in range(1, world)]
         else:
-            deadline = time.time() + timeout
             while True:
                 try:
-                    self._conn = Client((addr, port), authkey=authkey)
+                    c = socket.create_connection((addr, port), timeout=min(10.0, timeout))
                     break
-                except (ConnectionRefusedError, FileNotFoundError, OSError):
+                except OSError:
                     if time.time() > deadline:
                         raise
                     time.sleep(0.05)
-            self._conn.send(rank)
+            c.settimeout(timeout)
+            challenge = _recv_exact(c, 32)
+            c.sendall(rank.to_bytes(4, "little") + _mac(self._key, challenge, rank))
+            if _recv_exact(c, 2) != b"ok":
+                c.close()
+                raise ConnectionError("HostGroup: rank 0 refused this rank")
+            self._conn = c
+
+    def _admit(self, c, peers: dict):
+        """Challenge one connection; its rank if admitted, else None."""
+        import hmac
+        import socket
+
+        try:
+            c.settimeout(10.0)
+            challenge = os.urandom(32)
+            c.sendall(challenge)
+            msg = _recv_exact(c, 36)
+            r = int.from_bytes(msg[:4], "little")
+            if not (1 <= r < self.world) or r in peers or not hmac.compare_digest(msg[4:], _mac(self._key, challenge, r)):
+                return None
+            c.sendall(b"ok")
+            c.settimeout(self._timeout)
+            return r
+        except (OSError, socket.timeout, ConnectionError):
+            return None
 
     @staticmethod
     def from_env(offset: int = 1) -> "HostGroup":
         """RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT as torch.distributed.run
         sets them; the group listens on MASTER_PORT + offset (the launcher's
-        own store holds MASTER_PORT)."""
+        own store holds MASTER_PORT).  On a single-node launch (LOCAL_WORLD_SIZE
+        == WORLD_SIZE) rank 0 binds the loopback interface only."""
         rank = int(os.environ.get("RANK", "0"))
         world = int(os.environ.get("WORLD_SIZE", "1"))
         addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = int(os.environ.get("MASTER_PORT", "29500")) + offset
-        return HostGroup(rank, world, addr, port)
+        single_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+        bind = "127.0.0.1" if single_node else addr
+        if single_node:
+            addr = "127.0.0.1"
+        return HostGroup(rank, world, addr, port, bind_addr=bind)
+
+    # -- framing
+    @staticmethod
+    def _send(c, obj) -> None:
+        data = json.dumps(_enc(obj), separators=(",", ":")).encode()
+        c.sendall(len(data).to_bytes(8, "little") + data)
+
+    def _recv(self, c):
+        n = int.from_bytes(_recv_exact(c, 8), "little")
+        if n > self._MAX_FRAME:
+            raise ConnectionError(f"HostGroup: frame of {n} bytes exceeds {self._MAX_FRAME}")
+        return _dec(json.loads(_recv_exact(c, n)))
 
     def allgather(self, obj: Any) -> list:
         if self.world == 1:
             return [obj]
         if self.rank == 0:
-            out = [obj] + [c.recv() for c in self._peers]
+            out = [obj] + [self._recv(c) for c in self._peers]
             for c in self._peers:
-                c.send(out)
+                self._send(c, out)
             return out
-        self._conn.send(obj)
-        return self._conn.recv()
+        self._send(self._conn, obj)
+        return self._recv(self._conn)
 
     def broadcast(self, obj: Any = None) -> Any:
         """rank 0's obj on every rank."""
@@ -97,9 +169,9 @@ class HostGroup:
             return obj
         if self.rank == 0:
             for c in self._peers:
-                c.send(obj)
+                self._send(c, obj)
             return obj
-        return self._conn.recv()
+        return self._recv(self._conn)
 
     def barrier(self) -> None:
         self.allgather(None)
@@ -115,6 +187,67 @@ class HostGroup:
         if self._listener is not None:
             self._listener.close()
         self._peers, self._conn, self._listener = [], None, None
+
+
+def _launch_key(port: int) -> bytes:
+    explicit = os.environ.get("ECGPU_HOSTGROUP_KEY")
+    if explicit:
+        return hashlib.sha256(explicit.encode()).digest()
+    run = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    return hashlib.sha256(f"ecgpu-hostgroup|{run}|{port}".encode()).digest()
+
+
+def _mac(key: bytes, challenge: bytes, rank: int) -> bytes:
+    import hmac
+
+    return hmac.new(key, challenge + rank.to_bytes(4, "little"), hashlib.sha256).digest()
+
+
+def _recv_exact(c, n: int) -> bytes:
+    buf = bytearray()
+    while len(buf) < n:
+        chunk = c.recv(n - len(buf))
+        if not chunk:
+            raise ConnectionError("HostGroup: peer closed the connection")
+        buf += chunk
+    return bytes(buf)
+
+
+def _enc(o):
+    if o is None or isinstance(o, (bool, int, float, str)):
+        return o
+    if isinstance(o, (bytes, bytearray)):
+        return {"$b": bytes(o).hex()}
+    if isinstance(o, (list, tuple)):
+        return [_enc(x) for x in o]
+    if isinstance(o, dict) and all(isinstance(k, str) and not k.startswith("$") for k in o):
+        return {k: _enc(v) for k, v in o.items()}
+    mod = type(o).__module__
+    if mod == "numpy" and type(o).__name__ == "ndarray":  # plain numeric arrays: dtype, shape, bytes
+        if o.dtype.kind not in "biuf":
+            raise TypeError(f"HostGroup carries numeric arrays only, not dtype {o.dtype}")
+        return {"$a": [o.dtype.str, list(o.shape), o.tobytes().hex()]}
+    if mod == "numpy" and hasattr(o, "item"):  # numpy scalars
+        return _enc(o.item())
+    raise TypeError(f"HostGroup carries plain values only, not {type(o).__name__}")
+
+
+def _dec(o):
+    if isinstance(o, list):
+        return [_dec(x) for x in o]
+    if isinstance(o, dict):
+        if set(o) == {"$b"}:
+            return bytes.fromhex(o["$b"])
+        if set(o) == {"$a"}:
+            import numpy as np
+
+            dt, shape, hx = o["$a"]
+            dtype = np.dtype(dt)
+            if dtype.kind not in "biuf":
+                raise ValueError(f"HostGroup: refused array dtype {dt!r}")
+            return np.frombuffer(bytes.fromhex(hx), dtype=dtype).reshape(shape).copy()
+        return {k: _dec(v) for k, v in o.items()}
+    return o
 
 
 def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
@@ -161,17 +294,20 @@ def msm_sharded(n: int, partial_fn: Callable[[int, int], "object"], fold_fn: Cal
 
 
 def comm_init(prog, rank: int, world: int, broadcast: Callable[[Any], Any] | None = None,
-              make_id: Callable[[], bytes] | None = None) -> None:
+              make_id: Callable[[], bytes] | None = None) -> bytes:
     """Rank 0 makes the RCCL id (make_id, default ecg_comm_unique_id), the
     launcher's group broadcasts it (broadcast(obj) -> rank 0's obj, e.g.
     HostGroup.broadcast), every rank binds its Program's context
     (ecg_comm_init).  make_id is injectable so the CPU tests run the same
-    exchange without RCCL."""
+    exchange without RCCL.  Returns the 128-byte id every rank used."""
     import ctypes
 
     import ecgpu
 
     buf = (ctypes.c_uint8 * 128)()
+    if world > 1 and broadcast is None:
+        raise ValueError("comm_init: world > 1 needs a broadcast(obj) -> rank 0's obj callable "
+                         "(e.g. HostGroup.from_env().broadcast)")
     if world > 1:
         ident = None
         if rank == 0:

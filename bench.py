@@ -60,6 +60,7 @@ KAT_A = 0x1234567890ABCDEF1122334455667788
 KAT_B = 0x0FEDCBA987654321
 # reduced-radix limbs of the MSM's Fq (fieldrr.hpp): 14 x 29 bits (BLS12-381), 10 x 28 (BN254)
 RR_LIMBS = {0: 14, 1: 10}
+RR_BITS = {0: 29, 1: 28}
 FR_RR_MADS = 2 * 9 * 9         # v_mad_u64_u32 per reduced-radix Fr product (9 x 29-bit limbs, ntt.hip)
 
 
@@ -540,7 +541,7 @@ def main():
         achieved = n_acc * W * mads / (acc_avg_ms / 1e3) / 1e12
         roofline.update({"achieved": achieved, "peak": MAD_PEAK_T, "unit": "T v_mad_u64_u32/s",
                          "frac": achieved / MAD_PEAK_T,
-                         "note": f"{mads} v_mad_u64_u32 per XYZZ mixed add (8M+2S, {RR_LIMBS[cid]} x 29-bit limbs) "
+                         "note": f"{mads} v_mad_u64_u32 per XYZZ mixed add (8M+2S, {RR_LIMBS[cid]} x {RR_BITS[cid]}-bit limbs) "
                                  f"x {W} windows x terms / launch time; peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz"})
     roofline["hbm"] = {"achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": hbm_achieved / HBM_PEAK_GBS,
@@ -558,7 +559,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": ("mod-p integer on v_mad_u64_u32 (reduced-radix Montgomery: MSM Fq "
-                  + ("14 x 29-bit" if cid == 0 else "10 x 28-bit") + " limbs, NTT Fr 9 x 29-bit)"),
+                  + f"{RR_LIMBS[cid]} x {RR_BITS[cid]}-bit" + " limbs, NTT Fr 9 x 29-bit)"),
         "data": "synthetic: bases (a+i*b)G generated on GPU, scalars uniform < r (seeded), HBM-resident"
                 + ("" if args.unprepared else "; bases prepared once in the kernels' 128-B record layout "
                    "(ecg_msm_prepare_bases, upload_multiexp_bases's role)"),
@@ -614,22 +615,21 @@ def _g2_kat(cid: int, scal: np.ndarray, r_int: int, got: np.ndarray) -> bool:
 
 def pmc_traffic(kernel: str, streaming_read: bool):
     """HBM bytes per launch (GB) from the committed rocprofv3 PMC passes
-    (tools/gpu.sh prof -> profiles/<round>/pmc_fetch_write.json): FETCH_SIZE +
-    WRITE_SIZE.  gfx950 FETCH_SIZE counts half the bytes of wide coalesced
-    streaming reads (MI355X_MICROARCH.md, HBM/rocprofv3 section), so those are
-    doubled; gathers are reported as counted."""
-    import glob
-
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_fetch_write.json")))
-    if not files:
+    (tools/gpu.sh prof -> profiles/<round>/pmc_fetch_write.json, copied to
+    profiles/pmc_current.json with its source): FETCH_SIZE + WRITE_SIZE.
+    gfx950 FETCH_SIZE counts half the bytes of wide coalesced streaming reads
+    (MI355X_MICROARCH.md, HBM/rocprofv3 section), so those are doubled;
+    gathers are reported as counted."""
+    path = os.path.join(ROOT, "profiles", "pmc_current.json")
+    if not os.path.exists(path):
         return None, None
-    with open(files[-1]) as f:
+    with open(path) as f:
         d = json.load(f)
-    for k, v in d.items():
+    for k, v in d["kernels"].items():
         if kernel in k:
             fetch = v["FETCH_SIZE"]["mean_kb"] * 1024 / 1e9
             write = v["WRITE_SIZE"]["mean_kb"] * 1024 / 1e9
-            return (2 * fetch if streaming_read else fetch) + write, os.path.relpath(files[-1], ROOT)
+            return (2 * fetch if streaming_read else fetch) + write, d["source"]
     return None, None
 
 

@@ -145,7 +145,8 @@ int ecg_msm(ecg_ctx *ctx, int curve_id, const uint64_t *bases_xy, const uint64_t
 /* MultiexpKernel::parallel_multiexp + multiexp (multiexp.rs:324-400):
  * contiguous ceil(n / nctx) ranges, one host thread per context, each range
  * in device passes of at most ecg_msm_chunk_size terms, first error wins
- * (the other workers stop at their next pass), partial sums folded on the
+ * (every worker polls it before each of its passes, as it polls abort_cb, and
+ * stops with the first error), partial sums folded on the
  * host (multiexp.rs:394-397).  A context listed twice is used by one thread
  * at a time (every call holds its context's lock). */
 int ecg_msm_multi(ecg_ctx **ctxs, int nctx, int curve_id, const uint64_t *bases_xy,
@@ -165,10 +166,18 @@ int ecg_msm_dev(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_s
  * bucket kernels gather (G1: 128-B reduced-radix records; G2: [x, y]) and
  * returns it in *d_prepared.  Pass *d_prepared as d_bases to ecg_msm_dev,
  * ecg_multiple_multiexp or ecg_msm_dist (any call reading at most n bases of
- * the same curve): those calls then skip the per-call conversion.  The
- * buffer is immutable (re-prepare after changing the bases); release it
- * with ecg_dev_free. */
+ * the same curve): those calls then skip the per-call conversion.  A
+ * pointer k records into the buffer (k x the per-base record size, e.g. a
+ * rank's shard) reads bases k.. in the same form; a pointer inside it that
+ * is not on a record boundary is refused.  The buffer belongs to its device,
+ * not to ctx: any context on that device may use it.  It is immutable
+ * (re-prepare after changing the bases); release it with ecg_dev_free (on
+ * any context) -- never with hipFree. */
 int ecg_msm_prepare_bases(ecg_ctx *ctx, int curve_id, const void *d_bases, size_t n, void **d_prepared);
+/* Bytes per base in a prepared buffer (window_bits = 0: plain records;
+ * else the window table of that window size): the stride of base-aligned
+ * pointers into it.  0 for an unknown curve or a table form the curve lacks. */
+size_t ecg_msm_prepared_stride(int curve_id, uint32_t window_bits);
 
 /* Fixed-base form of ecg_msm_prepare_bases for bases reused across many
  * MSMs (upload_multiexp_bases's use in ag-cuda-ec, multiexp.rs:11-19): also
@@ -231,6 +240,22 @@ int ecg_msm_ex(ecg_ctx *ctx, int curve_id, const void *bases, int bases_layout, 
                const uint64_t *density, int cache_bases, uint64_t *out_jac, ecg_abort_cb abort_cb,
                void *user);
 void ecg_base_cache_clear(ecg_ctx *ctx);
+/* Host addresses of the bases arrays currently held by ctx's base cache
+ * (at most 8 entries, oldest first; the oldest is evicted by a new one):
+ * writes up to cap of them to out and returns how many are cached.  Lets a
+ * binding release its references to arrays the cache no longer holds. */
+size_t ecg_base_cache_keys(ecg_ctx *ctx, const void **out, size_t cap);
+
+/* The plan of a one-task MSM of n terms on curve_id -- ecg_msm_dev's
+ * (window_bits = 0) or ecg_multiple_multiexp's with num_chunks = 1 and the
+ * window pinned to window_bits: window bits c, windows W = ceil((|r| + 1) / c)
+ * and how the per-window bucket entries are sorted.  Not in the reference
+ * API: tests use it to assert which pipeline branch a case exercises. */
+#define ECG_SORT_GLOBAL 0   /* one sort over (group, bucket) keys            */
+#define ECG_SORT_PW_ONE 1   /* window-padded blocks, one sort over all blocks */
+#define ECG_SORT_PW_BLOCK 2 /* window-padded blocks, one sort per block      */
+int ecg_msm_plan_info(int curve_id, size_t n, uint32_t window_bits, uint32_t *c, uint32_t *windows,
+                      int *sort_mode);
 
 /* Sum `count` Jacobian points (3 x Lq u64 each, device memory) into one
  * normalised Jacobian point: the EC fold that follows the RCCL all-gather of

@@ -32,6 +32,11 @@ pub const ECG_ERR_RCCL: c_int = -5;
 pub const ECG_BASES_XY: c_int = 0;
 pub const ECG_BASES_ARK_AFFINE: c_int = 1;
 
+// ---- ecg_msm_plan_info sort modes ---------------------------------------------
+pub const ECG_SORT_GLOBAL: c_int = 0;
+pub const ECG_SORT_PW_ONE: c_int = 1;
+pub const ECG_SORT_PW_BLOCK: c_int = 2;
+
 /// `typedef int (*ecg_abort_cb)(void *user)`: polled between FFT passes and
 /// MSM device passes (the reference's `maybe_abort`, fft.rs:94-98,
 /// multiexp.rs:140-144).
@@ -87,6 +92,7 @@ extern "C" {
                                  d_prepared: *mut *mut c_void) -> c_int;
     pub fn ecg_msm_prepare_table(ctx: *mut ecg_ctx, curve_id: c_int, d_bases: *const c_void, n: usize,
                                  window_bits: u32, d_prepared: *mut *mut c_void) -> c_int;
+    pub fn ecg_msm_prepared_stride(curve_id: c_int, window_bits: u32) -> usize;
     pub fn ecg_msm_table_window(curve_id: c_int, n: usize) -> u32;
     pub fn ecg_multiple_multiexp(ctx: *mut ecg_ctx, curve_id: c_int, d_bases: *const c_void, n_bases: usize,
                                  scalars: *const u64, scalars_on_device: c_int, scalars_montgomery: c_int,
@@ -99,6 +105,9 @@ extern "C" {
                       density: *const u64, cache_bases: c_int, out_jac: *mut u64, abort_cb: ecg_abort_cb,
                       user: *mut c_void) -> c_int;
     pub fn ecg_base_cache_clear(ctx: *mut ecg_ctx);
+    pub fn ecg_base_cache_keys(ctx: *mut ecg_ctx, out: *mut *const c_void, cap: usize) -> usize;
+    pub fn ecg_msm_plan_info(curve_id: c_int, n: usize, window_bits: u32, c: *mut u32, windows: *mut u32,
+                             sort_mode: *mut c_int) -> c_int;
     pub fn ecg_point_sum_dev(ctx: *mut ecg_ctx, curve_id: c_int, d_points: *const c_void, count: usize,
                              out_jac: *mut u64, stream: *mut c_void) -> c_int;
     pub fn ecg_point_sum(curve_id: c_int, points: *const u64, count: usize, out_jac: *mut u64) -> c_int;

@@ -130,14 +130,17 @@ def test_inverse_round_trip_2p22(kernels):
         assert y == x * n % f.modulus
 
 
-def test_fft_2p24_matches_parallel_fft(kernels):
-    """BASELINE config (2): Fr NTT 2^24 on one MI355X, bit-exact vs CPU parallel_fft."""
-    f = po.BLS12_381_FR
+@pytest.mark.parametrize("fname,fid", FIELDS)
+def test_fft_2p24_matches_parallel_fft(kernels, fname, fid):
+    """BASELINE config (2) and config (5)'s Fr NTT: 2^24 on one MI355X,
+    bit-exact vs CPU parallel_fft (tests/fft.rs:86-176 runs the production
+    path against the CPU at its largest size), for BLS12-381 and BN254 Fr."""
+    f = po.FIELDS[fname]
     log_n = 24
-    a = rand_mont(f, 1 << log_n, 24)
+    a = rand_mont(f, 1 << log_n, 24 + fid)
     om = co.u64arr([f.to_mont(f.omega(1 << log_n))], 4)[0]
-    ref = co.parallel_fft(0, a, om, log_n, 4)
-    kernels["bls12_381_fr"].radix_fft(a, om, log_n)
+    ref = co.parallel_fft(fid, a, om, log_n, 4)
+    kernels[fname].radix_fft(a, om, log_n)
     assert (a == ref).all()
 
 

@@ -104,16 +104,29 @@ def test_msm_ragged_sizes(kernels, cname, cid):
 
 @pytest.mark.parametrize("cname,cid", CURVES)
 def test_msm_ragged_window_padded(kernels, cname, cid):
-    """Sizes >= 2^16 take the window-padded key path (one sort per window
-    block, blocks padded to the 128-entry segment with sentinels): ragged
-    sizes put padding and zero digits inside segments and between blocks."""
+    """Sizes >= 2^16 take the window-padded key path (blocks padded to the
+    128-entry segment with sentinels); at these sizes c <= 16, so every block
+    goes through ONE sort over all blocks (ECG_SORT_PW_ONE, asserted below;
+    the per-block sort is test_msm_per_block_sort_pinned_window's and the
+    2^24 KAT's).  Ragged sizes put padding and zero digits inside segments and
+    between blocks."""
     cv = po.CURVES[cname]
     for n in ((1 << 16) + 1, (1 << 16) + 37, 3 * (1 << 16) - 5):
+        assert ecgpu.msm_plan(cname, n)[2] == "pw_one", n
         B = co.gen_bases(cid, 1300 + n, 7, n, 8)
         E = rand_scalars(cv, n, n)
         E[::97] = 0  # zero scalars: sentinel entries in every window block
         assert same_point(cid, kernels[cname].multiexp(ecgpu.Worker(), B, E, 0),
                           co.multiexp_cpu(cid, B, E, nthreads=16)), n
+
+
+def test_plan_c_matches_library():
+    """plan_c below restates make_plan's cost model for the test ids; the
+    library's own plan (ecg_msm_plan_info) must agree."""
+    for cname, cid in CURVES:
+        nbits = 255 if cid == 0 else 254
+        for lg in range(16, 27):
+            assert ecgpu.msm_plan(cname, 1 << lg)[0] == plan_c(1 << lg, nbits), (cname, lg)
 
 
 def plan_c(n, nbits):
@@ -373,3 +386,74 @@ def test_msm_equal_and_opposite_bases(gpu_programs, cname, cid):
         Ee = np.ascontiguousarray(np.tile(E[0], (n, 1)))
         out = ecgpu.msm_dev(prog, cname, ecgpu.DeviceBuffer.upload(prog, Bn), ecgpu.DeviceBuffer.upload(prog, Ee), n)
         assert aff(cid, out) is None, n
+
+
+HEADLINE = [pytest.param(name, cid, id=f"{name}-2p24-c%d-W%d-%s" % ecgpu.msm_plan(name, 1 << 24))
+            for name, cid in CURVES]
+
+
+@pytest.mark.parametrize("cname,cid", HEADLINE)
+def test_msm_kat_2p24_headline_plan(gpu_programs, cname, cid):
+    """The bench headline's exact code path at 2^24: c = 20, W = 13 windows,
+    one 2-pass sort per window block (ECG_SORT_PW_BLOCK, msm_core_impl),
+    prepared 128-B records, device-resident scalars -- against the known
+    answer (sum s_i (a + i b) mod r) G.  Also a base-aligned view into the
+    prepared buffer (one rank's shard, as ecg_msm_dist receives it) against
+    the same MSM over unprepared bases.  Reference: tests/multiexp.rs:38-105
+    runs the production path at its largest size."""
+    assert ecgpu.msm_plan(cname, 1 << 24) == (20, 13, "pw_block")
+    cv = po.CURVES[cname]
+    prog = gpu_programs[0][0]
+    n = 1 << 24
+    a, b = 0x5EED2424, 0x1F2E3D
+    E = rand_scalars_np(cv, n, 2424 + cid)
+    d_b = ecgpu.gen_bases_dev(prog, cname, a, b, n)
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    prep = ecgpu.prepare_bases(prog, cname, d_b, n)
+    out = ecgpu.msm_dev(prog, cname, prep, d_e, n)
+    assert normalised_form_ok(cid, out)
+    kat = co.kat_scalar(cid, a, b, E, nthreads=16)
+    assert same_point(cid, out, co.gen_mul(cid, kat))
+    # shard 3 of 4 through a view of the prepared records vs the raw bases
+    lq = cv.fq.limbs64
+    q0, m = 3 * (n // 4), n // 4
+    view = prep.view(q0, m)
+    d_e_sh = ecgpu.DeviceBuffer.upload(prog, np.ascontiguousarray(E[q0:]))
+    got = ecgpu.msm_dev(prog, cname, view, d_e_sh, m)
+    want = np.zeros(3 * lq, np.uint64)
+    ecgpu._check(ecgpu.lib().ecg_msm_dev(prog.handle, cid, ctypes.c_void_p(d_b.ptr.value + q0 * 2 * lq * 8),
+                                         d_e_sh.ptr, m, want.ctypes.data_as(ctypes.c_void_p), 0, None))
+    assert same_point(cid, got, want)
+    kat_sh = co.kat_scalar(cid, (a + q0 * b) % cv.fr.modulus, b, np.ascontiguousarray(E[q0:]), nthreads=16)
+    assert same_point(cid, got, co.gen_mul(cid, kat_sh))
+    for buf in (prep, d_b, d_e, d_e_sh):
+        buf.free()
+
+
+PINNED = [pytest.param(name, cid, n, id=f"{name}-n{n}") for name, cid in CURVES
+          for n in ((1 << 16) + 37, 1 << 17)]
+
+
+@pytest.mark.parametrize("cname,cid,n", PINNED)
+def test_msm_per_block_sort_pinned_window(gpu_programs, cname, cid, n):
+    """One sort per window block (ECG_SORT_PW_BLOCK: c + log2 W > 20) at sizes
+    multiexp_cpu checks in seconds: multiple_multiexp with one chunk and the
+    window pinned to 17..20 (ag-cuda-ec/src/multiexp.rs:21-81, window_size),
+    over raw and prepared bases, with zero scalars in every block."""
+    cv = po.CURVES[cname]
+    prog = gpu_programs[0][0]
+    B = co.gen_bases(cid, 4100 + n, 9, n, 16)
+    E = rand_scalars_np(cv, n, 17 + n + cid)
+    E[::61] = 0
+    cpu = co.multiexp_cpu(cid, B, E, nthreads=16)
+    d_b = ecgpu.DeviceBuffer.upload(prog, B)
+    prep = ecgpu.prepare_bases(prog, cname, d_b, n)
+    for w in (17, 18, 19, 20):
+        assert ecgpu.msm_plan(cname, n, w) == (w, -(-(cv.fr.bits + 1) // w), "pw_block"), w
+        for bases in (d_b, prep):
+            got = ecgpu.multiple_multiexp(prog, bases, E, 1, w, curve=cname, pin_window=True)
+            assert got.shape[0] == 1
+            assert normalised_form_ok(cid, got[0])
+            assert same_point(cid, got[0], cpu), (w, bases is prep)
+    prep.free()
+    d_b.free()

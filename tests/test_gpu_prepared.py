@@ -3,6 +3,8 @@ half of ag-cuda-ec's upload_multiexp_bases (ag-cuda-ec/src/multiexp.rs:11-19)
 -- bases converted once into the bucket kernels' layout, then consumed by
 msm_dev, multiple_multiexp and the multi-pass MSM.  Checker: multiexp_cpu on
 the same bases (and the unprepared device path)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -139,3 +141,61 @@ def test_prepared_errors(prog):
     pb.free()  # idempotent
     d_b.free()
     d_e.free()
+
+
+def test_prepared_registry_across_contexts_and_views(prog):
+    """The prepared-bases registry is process-wide and range-keyed: a buffer
+    prepared on one context is read as records from another context on the
+    same device, base-aligned pointers into it (views) read the bases from
+    there, a pointer off a record boundary is refused, and a buffer freed on
+    another context is unregistered (the address then reads as raw [x, y])."""
+    cid, cname = 0, "bls12_381"
+    cv = po.CURVES[cname]
+    n = 5000
+    B = co.gen_bases(cid, 61, 67, n, 8)
+    E = rand_scalars(cv, n, 71)
+    other = ecgpu.program(prog.device)  # a second context on the same GPU
+    d_b = ecgpu.DeviceBuffer.upload(prog, B)
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    pb = ecgpu.prepare_bases(prog, cname, d_b, n)
+    want = co.multiexp_cpu(cid, B, E, nthreads=8)
+    assert same(cid, ecgpu.msm_dev(other, cname, pb, d_e, n), want)
+    # a view of bases [1000, 1000 + 3000) in the prepared form
+    v = pb.view(1000, 3000)
+    d_e2 = ecgpu.DeviceBuffer.upload(prog, np.ascontiguousarray(E[1000:4000]))
+    assert same(cid, ecgpu.msm_dev(other, cname, v, d_e2, 3000),
+                co.multiexp_cpu(cid, B[1000:4000], E[1000:4000], nthreads=8))
+    with pytest.raises(ecgpu.EcError, match="prepared bases"):  # from base 1000 the buffer holds n - 1000
+        ecgpu.msm_dev(prog, cname, pb.view(1000), d_e, n - 999)
+    odd = ecgpu.PreparedBases(prog, ctypes.c_void_p(pb.ptr.value + 64), cid, 10)
+    with pytest.raises(ecgpu.EcError, match="base boundary"):
+        ecgpu.msm_dev(prog, cname, odd, d_e, 10)
+    odd.ptr = None
+    assert pb.stride() == 128
+    # free through the other context: unregistered with its memory
+    ecgpu.lib().ecg_dev_free(other.handle, pb.ptr)
+    pb.ptr = None
+    # a prepared buffer released behind the library's back (hipFree of its
+    # allocation) and the address reused by raw [x, y] bases: the header nonce
+    # no longer matches, so the address reads as raw bases again
+    pb2 = ecgpu.prepare_bases(prog, cname, d_b, n)
+    hip = ctypes.CDLL(ecgpu.lib().ecg_runtime_info().decode().split("(")[1].split(")")[0])
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    hdr = 256  # msm.hip PREP_HEADER
+    ptr = pb2.ptr.value
+    prog.synchronize()
+    assert hip.hipFree(ctypes.c_void_p(ptr - hdr)) == 0
+    pb2.ptr = None
+    d_raw = ecgpu.DeviceBuffer(prog, n * 128 + hdr)
+    d_raw.write(np.concatenate([np.zeros(hdr // 8, np.uint64), B.reshape(-1)]))
+    if d_raw.ptr.value + hdr == ptr:  # the allocator handed the address back
+        raw_view = ecgpu.PreparedBases(prog, ctypes.c_void_p(ptr), cid, n)
+        out = np.zeros(18, np.uint64)
+        ecgpu._check(ecgpu.lib().ecg_msm_dev(prog.handle, cid, raw_view.ptr, d_e.ptr, n,
+                                             out.ctypes.data_as(ctypes.c_void_p), 0, None))
+        raw_view.ptr = None
+        assert same(cid, out, want)
+    d_raw.free()
+    for buf in (d_b, d_e, d_e2):
+        buf.free()
+    other.close()

@@ -31,6 +31,9 @@ for ctr, sub in (("FETCH_SIZE", f"pmc_fetch_{tag}"), ("WRITE_SIZE", f"pmc_write_
     shutil.copy(path, os.path.join(out_dir, f"pmc_{ctr.split('_')[0].lower()}_counters.csv"))
 with open(os.path.join(out_dir, "pmc_fetch_write.json"), "w") as f:
     json.dump(res, f, indent=1, sort_keys=True)
+# the copy bench.py reads on the GPU box (profiles/r*/ stays out of the gpurun push)
+with open(os.path.join(root, "profiles", "pmc_current.json"), "w") as f:
+    json.dump({"source": f"profiles/{tag}/pmc_fetch_write.json", "kernels": res}, f, indent=1, sort_keys=True)
 stats = os.path.join(root, "gpurun_out", f"prof_{tag}", "run_kernel_stats.csv")
 if os.path.exists(stats):
     shutil.copy(stats, os.path.join(out_dir, "kernel_stats.csv"))
