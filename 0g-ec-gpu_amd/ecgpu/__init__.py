@@ -35,7 +35,8 @@ LIB_PATH = os.environ.get("ECGPU_LIB") or os.path.join(os.path.dirname(_PKG), "l
 # ids shared with include/ecgpu.h
 FIELD_BLS12_381_FR, FIELD_BLS12_381_FQ, FIELD_BN254_FR, FIELD_BN254_FQ = 0, 1, 2, 3
 CURVE_BLS12_381, CURVE_BN254, CURVE_BLS12_381_G2, CURVE_BN254_G2 = 0, 1, 2, 3
-FIELD_NAMES = {"bls12_381_fr": 0, "bls12_381_fq": 1, "bn254_fr": 2, "bn254_fq": 3}
+FIELD_NAMES = {"bls12_381_fr": 0, "bls12_381_fq": 1, "bn254_fr": 2, "bn254_fq": 3,
+               "bls12_381_fq2": 4, "bn254_fq2": 5}  # the Fq2 ids are registry-only (add_field)
 CURVE_NAMES = {"bls12_381": 0, "bn254": 1, "bls12_381_g2": 2, "bn254_g2": 3}
 # u64 words per point coordinate (Fq for G1, Fq2 = [c0, c1] for G2)
 CURVE_FQ_LIMBS = {0: 6, 1: 4, 2: 12, 3: 8}
@@ -137,7 +138,17 @@ _SIGS = {
     "ecg_dev_free": (None, [ctypes.c_void_p, ctypes.c_void_p]),
     "ecg_dev_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     "ecg_dev_download": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
+    "ecg_device_info": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int),
+                                       ctypes.c_char_p, ctypes.c_size_t]),
+    "ecg_field_id": (ctypes.c_int, [_u64p, ctypes.c_size_t, ctypes.c_uint32]),
+    "ecg_curve_id": (ctypes.c_int, [_u64p, ctypes.c_size_t, ctypes.c_uint32, _u64p, ctypes.c_size_t]),
+    "ecg_has_kernel": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "ecg_field_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "ecg_curve_name": (ctypes.c_char_p, [ctypes.c_int]),
 }
+
+# ag_build::SourceBuilder request kinds (ECG_KIND_*)
+KIND_FIELD, KIND_FFT, KIND_EC, KIND_EC_FFT, KIND_MULTIEXP = 0, 1, 2, 3, 4
 
 
 def lib() -> ctypes.CDLL:
@@ -215,7 +226,10 @@ class SourceBuilder:
         return self
 
     def add_ec(self, curve: str) -> "SourceBuilder":
-        self.add_field(curve + "_fq").add_field(curve + "_fr")
+        family = curve[:-3] if curve.endswith("_g2") else curve
+        if curve.endswith("_g2"):
+            self.add_field(family + "_fq2")  # an extension field brings its sub-field (builder.rs:43-55)
+        self.add_field(family + "_fq").add_field(family + "_fr")
         self.ecs.add(curve)
         return self
 
@@ -246,18 +260,17 @@ class SourceBuilder:
 
 
 def generate(sb: SourceBuilder) -> None:
-    """ag_build::generate: validates that every requested instantiation is in
-    the prebuilt library (field/curve ids) and that the library loads."""
-    for f in sb.ffts:
-        if f not in ("bls12_381_fr", "bn254_fr"):
-            raise EcError(f"no prebuilt FFT for field {f!r}")
-    for c in sb.multiexps:
-        if c not in CURVE_NAMES:
-            raise EcError(f"no prebuilt multiexp for curve {c!r}")
-    for c in sb.ec_ffts:
-        if c not in CURVE_NAMES:
-            raise EcError(f"no prebuilt EC-FFT for curve {c!r}")
-    lib()
+    """ag_build::generate: checks every requested instantiation against the
+    loaded library's kernel registry (ecg_has_kernel), as the Rust ag_build
+    shim does at build time; an unserved request raises."""
+    L = lib()
+    requests = ([(KIND_FIELD, f, FIELD_NAMES) for f in sb.fields] + [(KIND_FFT, f, FIELD_NAMES) for f in sb.ffts]
+                + [(KIND_EC, c, CURVE_NAMES) for c in sb.ecs] + [(KIND_EC_FFT, c, CURVE_NAMES) for c in sb.ec_ffts]
+                + [(KIND_MULTIEXP, c, CURVE_NAMES) for c in sb.multiexps])
+    what = {KIND_FIELD: "field", KIND_FFT: "FFT", KIND_EC: "curve", KIND_EC_FFT: "EC-FFT", KIND_MULTIEXP: "multiexp"}
+    for kind, name, ids in requests:
+        if name not in ids or not L.ecg_has_kernel(kind, ids[name]):
+            raise EcError(f"no prebuilt {what[kind]} kernel for {name!r}")
 
 
 # ---------------------------------------------------------------------------
@@ -273,8 +286,20 @@ class Device:
     def all() -> list["Device"]:
         return [Device(i) for i in range(lib().ecg_device_count())]
 
+    def _info(self):
+        mem, cus, name = ctypes.c_size_t(), ctypes.c_int(), ctypes.create_string_buffer(256)
+        _check(lib().ecg_device_info(self.index, ctypes.byref(mem), ctypes.byref(cus), name, 256), "device_info")
+        return mem.value, cus.value, name.value.decode()
+
     def name(self) -> str:
-        return f"MI355X #{self.index} (gfx950)"
+        return f"#{self.index} {self._info()[2]}"
+
+    def memory(self) -> int:
+        """Device::memory (bytes of HBM)."""
+        return self._info()[0]
+
+    def compute_units(self) -> int:
+        return self._info()[1]
 
 
 class Program:

@@ -89,6 +89,41 @@ int ecg_ctx_set_msm_chunk(ecg_ctx *ctx, size_t max_terms);
 const char *ecg_runtime_info(void);
 const char *ecg_last_error(void);
 const char *ecg_version(void);
+/* rust_gpu_tools::Device's queries for one device without a context
+ * (Device::name / memory / compute_units, used by multiexp.rs:109-127):
+ * name gets the marketing name and gfx arch, NUL-terminated in name_cap bytes. */
+int ecg_device_info(int device, size_t *mem_bytes, int *compute_units, char *name, size_t name_cap);
+
+/* ---- kernel registry --------------------------------------------------------
+ * The HIP kernels are compiled into this library ahead of time, so the
+ * reference's build-time code generator (ag_build::SourceBuilder::{add_field,
+ * add_fft, add_ec, add_ec_fft, add_multiexp} + generate, ag-build/src/
+ * source/builder.rs:43-99, lib.rs:47-53) becomes a query of which
+ * instantiations the library holds.  Fields and curves are named by their
+ * moduli, exactly what ag_types::GpuField::modulus() / ark_ff::Field::
+ * characteristic() report (ag-types/src/lib.rs:33-50), so a generic kernel
+ * needs no extra trait bound to find its id.  Moduli are little-endian u64
+ * limbs (high zero limbs ignored); degree is the extension degree over the
+ * prime field (1, or 2 for the G2 coordinate field Fq2). */
+#define ECG_FIELD_BLS12_381_FQ2 4 /* registry only: add_field::<Fq2>  */
+#define ECG_FIELD_BN254_FQ2 5
+#define ECG_KIND_FIELD 0    /* add_field    -> field id  */
+#define ECG_KIND_FFT 1      /* add_fft      -> field id  */
+#define ECG_KIND_EC 2       /* add_ec       -> curve id  */
+#define ECG_KIND_EC_FFT 3   /* add_ec_fft   -> curve id  */
+#define ECG_KIND_MULTIEXP 4 /* add_multiexp -> curve id  */
+/* field id, or ECG_ERR_INVALID (last error names the modulus) */
+int ecg_field_id(const uint64_t *modulus, size_t limbs, uint32_t degree);
+/* curve id from the coordinate field (base_degree 1 = G1, 2 = G2) and the
+ * scalar field, or ECG_ERR_INVALID */
+int ecg_curve_id(const uint64_t *base_modulus, size_t base_limbs, uint32_t base_degree,
+                 const uint64_t *scalar_modulus, size_t scalar_limbs);
+/* 1 if the library holds kernels of `kind` for id (a field id for FIELD/FFT,
+ * a curve id otherwise), else 0 */
+int ecg_has_kernel(int kind, int id);
+/* "bls12_381_fr", "bn254_g2", ...; NULL for an unknown id */
+const char *ecg_field_name(int field_id);
+const char *ecg_curve_name(int curve_id);
 
 /* ---- FFT ----------------------------------------------------------------
  * In-place forward DFT of size 2^log_n over field_id (an Fr), natural order

@@ -1,10 +1,9 @@
 //! Raw bindings to libecgpu.so: one `extern "C"` declaration per entry point of
-//! `include/ecgpu.h`, same order, same argument meaning.  Drop into
-//! `ec-gpu-proxy/src/amd/ffi.rs` (feature `amd`); `amd.rs` wraps it in the
-//! reference's types.  `tests/test_rust_shim.py` checks this file against the
-//! header (names, arity, pointer/scalar kinds, constants) so the two cannot
-//! drift; no Rust toolchain exists in the build image, so it is not compiled here.
-#![allow(non_camel_case_types, dead_code)]
+//! `include/ecgpu.h`, same order, same argument meaning.  The replacement
+//! crates of this workspace (rust-gpu-tools, ec-gpu-program, ag-build, the
+//! ec-gpu-proxy `amd` modules, ag-cuda-ec) wrap it in the reference's types.
+//! `tests/test_rust_shim.py` checks this file against the header (names,
+//! arity, pointer/scalar kinds, constants) so the two cannot drift.
 
 use std::os::raw::{c_char, c_int, c_void};
 
@@ -18,6 +17,15 @@ pub const ECG_CURVE_BLS12_381: c_int = 0;
 pub const ECG_CURVE_BN254: c_int = 1;
 pub const ECG_CURVE_BLS12_381_G2: c_int = 2;
 pub const ECG_CURVE_BN254_G2: c_int = 3;
+
+// ---- kernel registry (ag_build::SourceBuilder kinds) ------------------------
+pub const ECG_FIELD_BLS12_381_FQ2: c_int = 4;
+pub const ECG_FIELD_BN254_FQ2: c_int = 5;
+pub const ECG_KIND_FIELD: c_int = 0;
+pub const ECG_KIND_FFT: c_int = 1;
+pub const ECG_KIND_EC: c_int = 2;
+pub const ECG_KIND_EC_FFT: c_int = 3;
+pub const ECG_KIND_MULTIEXP: c_int = 4;
 
 // ---- return codes -----------------------------------------------------------
 pub const ECG_OK: c_int = 0;
@@ -61,6 +69,16 @@ extern "C" {
     pub fn ecg_runtime_info() -> *const c_char;
     pub fn ecg_last_error() -> *const c_char;
     pub fn ecg_version() -> *const c_char;
+    pub fn ecg_device_info(device: c_int, mem_bytes: *mut usize, compute_units: *mut c_int, name: *mut c_char,
+                           name_cap: usize) -> c_int;
+
+    // ---- kernel registry (ag-build/src/source/builder.rs:43-99, lib.rs:47-53) ----
+    pub fn ecg_field_id(modulus: *const u64, limbs: usize, degree: u32) -> c_int;
+    pub fn ecg_curve_id(base_modulus: *const u64, base_limbs: usize, base_degree: u32,
+                        scalar_modulus: *const u64, scalar_limbs: usize) -> c_int;
+    pub fn ecg_has_kernel(kind: c_int, id: c_int) -> c_int;
+    pub fn ecg_field_name(field_id: c_int) -> *const c_char;
+    pub fn ecg_curve_name(curve_id: c_int) -> *const c_char;
 
     // ---- FFT (fft.rs:50-135, 200-246) ----
     pub fn ecg_fft(ctx: *mut ecg_ctx, field_id: c_int, inout: *mut u64, omega: *const u64, log_n: u32,

@@ -92,6 +92,56 @@ def test_source_builder_and_generate():
         ecgpu.generate(ecgpu.SourceBuilder.new().add_ec_fft("bls12_377"))
 
 
+def _limbs(x: int) -> np.ndarray:
+    return np.array([(x >> (64 * i)) & (2**64 - 1) for i in range(max(1, (x.bit_length() + 63) // 64))],
+                    dtype=np.uint64)
+
+
+def test_kernel_registry_from_moduli():
+    """ecg_field_id / ecg_curve_id resolve an instantiation from the moduli
+    ag_types::GpuField::modulus() reports, as the Rust ag_build / program!
+    shims do (integration/rust/ecgpu-sys/src/lib.rs)."""
+    import py_oracle as po
+
+    L = ecgpu.lib()
+    fr, fq = po.BLS12_381_FR.modulus, po.BLS12_381_FQ.modulus
+    bfr, bfq = po.BN254_FR.modulus, po.BN254_FQ.modulus
+
+    def fid(p, degree=1, pad=0):
+        m = np.concatenate([_limbs(p), np.zeros(pad, np.uint64)])
+        return L.ecg_field_id(m.ctypes.data_as(ecgpu._u64p), len(m), degree)
+
+    assert fid(fr) == ecgpu.FIELD_BLS12_381_FR and fid(fr, pad=2) == ecgpu.FIELD_BLS12_381_FR
+    assert fid(fq) == ecgpu.FIELD_BLS12_381_FQ and fid(bfr) == ecgpu.FIELD_BN254_FR and fid(bfq) == ecgpu.FIELD_BN254_FQ
+    assert fid(fq, 2) == ecgpu.FIELD_NAMES["bls12_381_fq2"] and fid(bfq, 2) == ecgpu.FIELD_NAMES["bn254_fq2"]
+    assert fid(fr + 2) == ecgpu.ECG_ERR_INVALID and "modulus 0x73eda753" in ecgpu.last_error()
+    assert fid(fr, 2) == ecgpu.ECG_ERR_INVALID
+
+    def cid(base, degree, scalar):
+        b, sc = _limbs(base), _limbs(scalar)
+        return L.ecg_curve_id(b.ctypes.data_as(ecgpu._u64p), len(b), degree, sc.ctypes.data_as(ecgpu._u64p), len(sc))
+
+    assert cid(fq, 1, fr) == ecgpu.CURVE_BLS12_381 and cid(bfq, 1, bfr) == ecgpu.CURVE_BN254
+    assert cid(fq, 2, fr) == ecgpu.CURVE_BLS12_381_G2 and cid(bfq, 2, bfr) == ecgpu.CURVE_BN254_G2
+    assert cid(fq, 1, bfr) == ecgpu.ECG_ERR_INVALID and "no curve" in ecgpu.last_error()
+
+    K = ecgpu
+    assert L.ecg_has_kernel(K.KIND_FFT, K.FIELD_BLS12_381_FR) == 1 and L.ecg_has_kernel(K.KIND_FFT, K.FIELD_BN254_FR) == 1
+    assert L.ecg_has_kernel(K.KIND_FFT, K.FIELD_BLS12_381_FQ) == 0          # no 2-adic roots in Fq
+    for c in range(4):
+        for kind in (K.KIND_EC, K.KIND_EC_FFT, K.KIND_MULTIEXP):
+            assert L.ecg_has_kernel(kind, c) == 1
+    assert L.ecg_has_kernel(K.KIND_MULTIEXP, 7) == 0 and L.ecg_has_kernel(9, 0) == 0
+    assert L.ecg_field_name(0) == b"bls12_381_fr" and L.ecg_curve_name(3) == b"bn254_g2"
+    assert L.ecg_field_name(17) is None and L.ecg_curve_name(-1) is None
+
+
+def test_source_builder_g2_fields():
+    sb = ecgpu.SourceBuilder.new().add_multiexp("bls12_381_g2").add_ec_fft("bn254_g2")
+    assert {"bls12_381_fq2", "bls12_381_fq", "bls12_381_fr", "bn254_fq2", "bn254_fq"} <= sb.fields
+    ecgpu.generate(sb)
+
+
 def test_worker_threads_env(monkeypatch):
     monkeypatch.setenv("EC_GPU_NUM_THREADS", "12")   # threadpool.rs:25-30
     w = ecgpu.Worker()

@@ -1,20 +1,52 @@
-"""The Rust shim (integration/rust/) against the C ABI it binds (include/ecgpu.h).
+"""The Rust drop-in crates (integration/rust/) against the C ABI they bind
+(include/ecgpu.h) and against the reference's public Rust API.
 
-No Rust toolchain exists in the image, so the shim cannot be compiled here;
-these checks keep it from drifting from the header: every header function is
-declared in ffi.rs with the same arity, the same pointer / scalar kind per
-argument and the same return kind, every header constant has the same value,
-and every ffi:: call in amd.rs names a declared function with its arity.
+No Rust toolchain exists in the image, so the crates cannot be compiled here;
+these checks keep them from drifting:
+  * every header function is declared in ecgpu-sys's ffi.rs with the same
+    arity, pointer / scalar kind per argument and return kind, and every
+    header constant has the same value;
+  * every `sys::ecg_*` call in the crates names a declared function with its
+    arity;
+  * every public item of the reference's ec-gpu path -- structs with their
+    generics and bounds, methods and functions with their parameter lists and
+    return types, macros, error variants, re-exports, the `_st` / `_mt`
+    functions `#[auto_workspace]` generates -- exists in the drop-in with the
+    identical signature (tests/golden/rust_api.json, extracted from the
+    reference by tests/golden/make_rust_api.py).
 """
+import json
 import os
 import re
+import sys
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import rustsig as rs  # noqa: E402
+
 HEADER = os.path.join(ROOT, "include", "ecgpu.h")
-FFI = os.path.join(ROOT, "integration", "rust", "ffi.rs")
-AMD = os.path.join(ROOT, "integration", "rust", "amd.rs")
+RUST = os.path.join(ROOT, "integration", "rust")
+FFI = os.path.join(RUST, "ecgpu-sys", "src", "ffi.rs")
+API = os.path.join(ROOT, "tests", "golden", "rust_api.json")
+
+# module path -> the drop-in files that define it
+SHIM = {
+    "ec_gpu_proxy::fft": ["ec-gpu-proxy/src/amd/fft.rs"],
+    "ec_gpu_proxy::multiexp": ["ec-gpu-proxy/src/amd/multiexp.rs"],
+    "ec_gpu_proxy::ec_fft": ["ec-gpu-proxy/src/amd/ec_fft.rs"],
+    "ag_build": ["ag-build/src/lib.rs"],
+    "ec_gpu_program": ["ec-gpu-program/src/lib.rs"],
+    "ag_cuda_ec": ["ag-cuda-ec/src/lib.rs"],
+    "ag_cuda_ec::multiexp": ["ag-cuda-ec/src/multiexp.rs"],
+    "ag_cuda_ec::ec_fft": ["ag-cuda-ec/src/ec_fft.rs"],
+    "rust_gpu_tools": ["rust-gpu-tools/src/lib.rs"],
+}
+SHIM_FILES = sorted({os.path.join(RUST, f) for fs in SHIM.values() for f in fs}
+                    | {os.path.join(RUST, "ec-gpu-proxy/src/amd/mod.rs"),
+                       os.path.join(RUST, "ag-cuda-ec/src/workspace.rs"),
+                       os.path.join(RUST, "ecgpu-sys/src/lib.rs")})
 
 
 def _strip_c_comments(s):
@@ -114,28 +146,79 @@ def test_constants_match_header():
     assert consts and consts == rs
 
 
-@pytest.mark.parametrize("path", [AMD])
-def test_shim_calls_declared_functions_with_their_arity(path):
+def test_shim_calls_declared_functions_with_their_arity():
     decl = ffi_functions()
-    src = open(path).read()
     calls = 0
-    for m in re.finditer(r"ffi::(ecg_\w+)\(", src):
-        name = m.group(1)
-        assert name in decl, name
-        depth, i = 1, m.end()
-        while depth:
-            depth += {"(": 1, ")": -1}.get(src[i], 0)
-            i += 1
-        assert len(_split_args(src[m.end():i - 1])) == len(decl[name][1]), name
-        calls += 1
+    for path in SHIM_FILES:
+        src = open(path).read()
+        for m in re.finditer(r"\bsys::(ecg_\w+)\(", src):
+            name = m.group(1)
+            assert name in decl, (path, name)
+            depth, i = 1, m.end()
+            while depth:
+                depth += {"(": 1, ")": -1}.get(src[i], 0)
+                i += 1
+            assert len(_split_args(src[m.end():i - 1])) == len(decl[name][1]), (path, name)
+            calls += 1
     assert calls >= 15
 
 
-def test_shim_mirrors_reference_entry_points():
-    src = open(AMD).read()
-    for sym in ("pub struct FftKernel", "pub fn radix_fft_many", "pub struct MultiexpKernel",
-                "pub fn parallel_multiexp<'s>", "scope: &Scope<'s>", "pub fn multiexp(&mut self, pool: &Worker",
-                "pub fn num_kernels", "pub struct SingleMultiexpKernel", "pub struct EcFftKernel",
-                "pub fn radix_ec_fft_many", "pub fn upload_multiexp_bases", "pub fn multiple_multiexp",
-                "\"No working GPUs found!\"", "\"Expected more bases from source.\"", "EcError::Aborted"):
-        assert sym in src, sym
+def _shim_api(module):
+    apis = [rs.parse(open(os.path.join(RUST, f)).read()) for f in SHIM[module]]
+    return rs.merge(*apis)
+
+
+def _ref_items():
+    ref = json.load(open(API))["modules"]
+    for module, api in sorted(ref.items()):
+        for kind in ("structs", "methods", "fns"):
+            for name in sorted(api[kind]):
+                yield module, kind, name
+
+
+def test_signature_list_covers_the_path():
+    ref = json.load(open(API))["modules"]
+    assert set(ref) == set(SHIM)
+    methods = set(ref["ec_gpu_proxy::multiexp"]["methods"])
+    assert {"MultiexpKernel::create", "MultiexpKernel::create_with_abort", "SingleMultiexpKernel::create",
+            "MultiexpKernel::parallel_multiexp", "MultiexpKernel::multiexp"} <= methods
+    assert {"SourceBuilder::add_fft", "SourceBuilder::add_multiexp"} <= set(ref["ag_build"]["methods"])
+    assert {"multiple_multiexp_st", "multiple_multiexp_mt", "upload_multiexp_bases_st"} <= \
+        set(ref["ag_cuda_ec::multiexp"]["fns"])
+    assert {"radix_ec_fft_st", "radix_ec_fft_mt"} <= set(ref["ag_cuda_ec::ec_fft"]["fns"])
+    assert sum(1 for _ in _ref_items()) >= 55
+
+
+@pytest.mark.parametrize("module,kind,name", list(_ref_items()), ids=lambda x: str(x))
+def test_reference_item_has_identical_signature(module, kind, name):
+    want = json.load(open(API))["modules"][module][kind][name]
+    got = _shim_api(module)[kind].get(name)
+    assert got is not None, f"{module}: {kind[:-1]} {name} missing from the drop-in"
+    for field in ("generics", "params", "ret", "bounds"):
+        if field in want:
+            assert got[field] == want[field], f"{module}::{name} {field}: drop-in {got[field]!r} vs reference {want[field]!r}"
+
+
+@pytest.mark.parametrize("module", sorted(SHIM))
+def test_reference_macros_variants_and_reexports(module):
+    want = json.load(open(API))["modules"][module]
+    got = _shim_api(module)
+    assert set(want["macros"]) <= set(got["macros"]), set(want["macros"]) - set(got["macros"])
+    for enum, variants in want["enums"].items():
+        assert enum in got["enums"], enum
+        assert set(variants) <= set(got["enums"][enum]), (enum, set(variants) - set(got["enums"][enum]))
+    names = set(got["uses"]) | set(got["structs"]) | set(got["enums"])
+    assert set(want["uses"]) <= names, set(want["uses"]) - names
+
+
+def test_parser_sees_a_drifted_signature():
+    """The comparison is not vacuous: dropping `devices` from the constructor
+    (the round-2 drift) is caught."""
+    src = open(os.path.join(RUST, "ec-gpu-proxy/src/amd/multiexp.rs")).read()
+    drifted = src.replace("programs: Vec<Program>, devices: &[&Device],\n    ) -> EcResult<Self> {\n"
+                          "        Self::create_optional_abort(programs, devices, None)",
+                          "programs: Vec<Program>,\n    ) -> EcResult<Self> {\n"
+                          "        Self::create_optional_abort(programs, &[], None)")
+    assert drifted != src
+    want = json.load(open(API))["modules"]["ec_gpu_proxy::multiexp"]["methods"]["MultiexpKernel::create"]
+    assert rs.parse(drifted)["methods"]["MultiexpKernel::create"]["params"] != want["params"]
