@@ -1,5 +1,14 @@
 """world_size-2 multi-process CPU tests of the N>1 path bench.py runs.
 
+* test_bench_main_world2: two processes run bench.main() itself under the
+  launcher's environment (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR /
+  MASTER_PORT, as torch.distributed.run sets them): HostGroup.from_env on
+  MASTER_PORT + 1, comm_init's id broadcast, the per-rank shards and seeds,
+  the barrier / max-over-ranks timing, rank 0's full-size KAT regeneration,
+  the distributed-NTT digest check and the rank-0-only JSON report.  Only the
+  device calls (program, DeviceBuffer, gen_bases_dev, prepare_bases, msm_dev,
+  fft_dev, msm_dist, fft_dist) are replaced, by CPU-oracle stand-ins that
+  exchange partials and blocks over a second HostGroup as RCCL would.
 * test_bench_dist_path_world2: two processes run bench.py's own host-side
   orchestration -- ecgpu.dist.HostGroup (the launch's control channel),
   comm_init's RCCL-id broadcast (with an injected id maker: no RCCL on CPU),
@@ -83,6 +92,143 @@ def test_bench_dist_path_world2():
     results = dict(q.get(timeout=10) for _ in range(2))
     assert all(p.exitcode == 0 for p in procs)
     assert results == {0: True, 1: True}
+
+
+class _FakeProg:
+    handle = None
+
+    def synchronize(self):
+        pass
+
+    def kernel_time(self, name):
+        return 0.25, 1
+
+
+class _FakeBuf:
+    """DeviceBuffer stand-in: the 'device' bytes are a numpy array."""
+
+    def __init__(self, arr):
+        self.arr = np.ascontiguousarray(arr, dtype=np.uint64).copy()
+        self.ptr = id(self)
+        self.nbytes = self.arr.nbytes
+
+    @staticmethod
+    def upload(prog, host):
+        return _FakeBuf(host)
+
+    def write(self, host):
+        self.arr[...] = np.asarray(host, dtype=np.uint64).reshape(self.arr.shape)
+
+    def read(self, dtype=np.uint64, shape=None):
+        out = self.arr.copy()
+        return out.reshape(shape) if shape is not None else out
+
+    def free(self):
+        self.ptr = None
+
+
+def _install_device_fakes(rank, world, corrupt=False):
+    """Swap ecgpu's device entry points for CPU-oracle stand-ins (checker-grade
+    results, so bench.main()'s own checks can pass or fail for real)."""
+    import coracle as co
+    import ecgpu
+    from ecgpu import dist as edist
+
+    side = edist.HostGroup.from_env(offset=2)  # the 'RCCL' of the stand-ins
+    real_comm_init = edist.comm_init
+    fid_of = {"bls12_381_fr": 0, "bn254_fr": 2}
+
+    def gen_bases_dev(prog, curve, a, b, n):
+        return _FakeBuf(co.gen_bases(ecgpu._curve(curve), int(a), int(b), n, 2))
+
+    def msm_local(curve, bases, scal, n):
+        cid = ecgpu._curve(curve)
+        nq = ecgpu.CURVE_FQ_LIMBS[cid]
+        if n == 0:
+            return np.concatenate([np.zeros(nq, np.uint64), co.u64arr([1], nq)[0], np.zeros(nq, np.uint64)])
+        return co.multiexp_cpu(cid, bases.arr.reshape(-1, 2 * nq)[:n], scal.arr.reshape(-1, 4)[:n],
+                               nthreads=2).reshape(-1)
+
+    def msm_dist(prog, curve, bases, scal, n_local):
+        cid = ecgpu._curve(curve)
+        parts = side.allgather(msm_local(curve, bases, scal, n_local))
+        return _fold(co, cid, parts)
+
+    def fft_dev(prog, field, d, omega, log_n):
+        d.arr[...] = co.serial_fft(fid_of[field], d.arr.reshape(-1, 4), np.asarray(omega, np.uint64), log_n)
+
+    def fft_dist(prog, field, d_local, omega, log_n):
+        blocks = side.allgather(d_local.arr.reshape(-1, 4))
+        full = co.serial_fft(fid_of[field], np.ascontiguousarray(np.concatenate(blocks)),
+                             np.asarray(omega, np.uint64), log_n)
+        m = full.shape[0] // world
+        d_local.arr[...] = full[rank * m:(rank + 1) * m]
+        if corrupt and rank == 1:
+            d_local.arr.reshape(-1)[5] ^= np.uint64(1)
+
+    ecgpu.Device = lambda i: i
+    ecgpu.program = lambda dev: _FakeProg()
+    ecgpu.DeviceBuffer = _FakeBuf
+    ecgpu.gen_bases_dev = gen_bases_dev
+    ecgpu.prepare_bases = lambda prog, curve, d, n, window_table=None: d
+    ecgpu.msm_dev = lambda prog, curve, b, s, n: msm_local(curve, b, s, n)
+    ecgpu.fft_dev = fft_dev
+    edist.comm_init = lambda prog, r, w, bcast: real_comm_init(None, r, w, bcast, make_id=lambda: bytes(range(128)))
+    edist.msm_dist = msm_dist
+    edist.fft_dist = fft_dist
+    return side
+
+
+def _bench_main_worker(rank, world, port, q, corrupt=False):
+    import contextlib
+    import io
+
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                       "OMP_NUM_THREADS": "2"})
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "0g-ec-gpu_amd"))
+    side = _install_device_fakes(rank, world, corrupt)
+    import bench
+
+    sys.argv = ["bench.py", "--gpus", str(world), "--steps", "2", "--warmup", "1", "--msm-log", "10",
+                "--ntt-log", "8"]
+    out = io.StringIO()
+    try:
+        with contextlib.redirect_stdout(out):
+            bench.main()
+    finally:
+        side.close()
+    q.put((rank, out.getvalue()))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("corrupt", [False, True], ids=["exact", "corrupted_block"])
+def test_bench_main_world2(corrupt):
+    """bench.main() end to end at N = 2 on CPU: the JSON line rank 0 prints
+    carries the full-size MSM KAT and the distributed-NTT digest check; one
+    flipped bit in rank 1's NTT block turns exactly that check false."""
+    import json
+    import multiprocessing as mp
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_main_worker, args=(r, 2, port, q, corrupt)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    outs = dict(q.get(timeout=10) for _ in range(2))
+    assert all(p.exitcode == 0 for p in procs)
+    assert outs[1] == ""  # only rank 0 reports
+    line = json.loads(outs[0].strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["config"]["msm_terms"] == 1 << 10
+    assert line["checks"] == {"msm_kat_2^10": True, "ntt_vs_parallel_fft_2^8": True,
+                              "ntt_dist_2gpu_vs_parallel_fft_2^8": not corrupt}
+    assert line["value"] > 0 and line["ntt_dist"]["value"] > 0
+    assert line["msm_window_table"]["equals_headline_result"] is True
 
 
 def test_kat_scalar_regeneration_matches_single_rank():

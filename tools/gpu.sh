@@ -49,11 +49,35 @@ sq() {
   python3 $R/tools/sq_summary.py $R/gpurun_out/sq_$TAG/run_counter_collection.csv | tee $R/gpurun_out/sq_${TAG}_summary.txt
 }
 
+# one counter pass over any python target: pmc TAG "CTR ..." script.py args...
+pmc() {
+  local TAG=$1 CTRS=$2; shift 2
+  ( cd /tmp && export TMPDIR=/tmp &&
+    timeout -s KILL 300 rocprofv3 --pmc $CTRS --kernel-trace -d $R/gpurun_out/pmc_$TAG -o run --output-format csv \
+      -- python3 "$@" > $R/gpurun_out/pmc_$TAG.log 2>&1 ) || { echo "pmc $TAG failed"; return 1; }
+  echo "pmc $TAG ok"
+}
+
+# diagnostics: in-kernel clock (GRBM) + SQ instruction mix of the MSM accumulate
+# (both curves) and of the NTT pass
+diag() {
+  local TAG=$1 SQ1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY"
+  local SQ2="SQ_WAVES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
+  pmc ${TAG}_clk_bls "GRBM_GUI_ACTIVE GRBM_COUNT" $R/tools/msm_once.py 26 16 1 bls12_381 &&
+  pmc ${TAG}_clk_bn "GRBM_GUI_ACTIVE GRBM_COUNT" $R/tools/msm_once.py 26 20 1 bn254 &&
+  pmc ${TAG}_sq_bls "$SQ1" $R/tools/msm_once.py 24 1 1 bls12_381 &&
+  pmc ${TAG}_sq_bn "$SQ1" $R/tools/msm_once.py 24 1 1 bn254 &&
+  pmc ${TAG}_clk_ntt "GRBM_GUI_ACTIVE GRBM_COUNT" $R/tools/ntt_once.py 24 1000 &&
+  pmc ${TAG}_sq_ntt "$SQ1" $R/tools/ntt_once.py 24 3 &&
+  pmc ${TAG}_sq2_ntt "$SQ2" $R/tools/ntt_once.py 24 3
+}
+
 case $cmd in
   tests) tests "$@" ;;
   bench) bench "$@" ;;
   prof) prof "$@" ;;
   sq) sq "$@" ;;
+  diag) diag "$@" ;;
   round)
     TAG=$1
     tests && bench && {
