@@ -1,7 +1,9 @@
 """Timing of the batched multi-line MSM on the shape of ag-cuda-ec/benches/
 amt.rs (LOG_N = 10: LENGTH = 2^21 scalars, 10 lines of bases, 2^7 .. 2^11
 chunks per line).  Dev tool; prints one JSON line per configuration.
-Usage: python tools/batch_bench.py [log_n] [--cycled]"""
+Usage: python tools/batch_bench.py [log_n] [--cycled] [--prepared] [--chunks=K]
+--prepared: bases converted once (upload_multiexp_bases); --chunks=K: only
+that chunk count."""
 import json
 import os
 import sys
@@ -27,9 +29,11 @@ else:
     E = rng.integers(0, 2**64, size=(L, 4), dtype=np.uint64)
     E[:, 3] &= np.uint64(2**62 - 1)
 d_b = ecgpu.gen_bases_dev(prog, "bls12_381", 99, 12345, L * lines)
+if "--prepared" in sys.argv:
+    d_b = ecgpu.prepare_bases(prog, "bls12_381", d_b, L * lines)
 d_e = ecgpu.DeviceBuffer.upload(prog, E)
-for gdeg in range(7, 12):
-    chunks = 1 << gdeg
+only = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--chunks=")]
+for chunks in only or [1 << gdeg for gdeg in range(7, 12)]:
     ecgpu.multiple_multiexp(prog, d_b, (d_e, L), chunks)
     best = 1e9
     for _ in range(3):
@@ -40,4 +44,4 @@ for gdeg in range(7, 12):
     terms = L * lines
     print(json.dumps({"lines": lines, "line_len": L, "chunks": chunks, "tasks": lines * chunks,
                       "chunk_len": L // chunks, "ms": round(best * 1e3, 2), "acc_ms": round(acc, 2),
-                      "terms_per_s": terms / best, "cycled": cycled}), flush=True)
+                      "terms_per_s": terms / best, "cycled": cycled, "prepared": "--prepared" in sys.argv}), flush=True)
