@@ -13,6 +13,24 @@
 //   add:   P, R <= 5.01 (+4p), the rest as madd
 //   dbl:   U = 2Y <= 8.02, M = 3X^2 <= 3.03, X3, Y3 as madd
 // Largest product of operand bounds: 65 x 65 = 4225 << 2^24.
+//
+// Tight-slack layouts (rr_tight: R'/p < 2^16 -- BN254's 9 x 29-bit G1 form,
+// R'/p ~ 167.8, chosen over 10 x 28 bits for 162 instead of 200 mads per
+// product) cannot afford those operands: a product output is
+// < a b / R' + p, so operands must multiply to well under 168 p^2.  There X3
+// is brought back to ~p by rr_reduce_q (a product-free "mod p, almost") and
+// every subtraction uses 4p, which bounds everything by:
+//   stored points  X <= 1.02 (reduced), Y <= 1.25, ZZ, ZZZ <= M;  M < 1.25 p
+//                  (largest product below 35 p^2); bases x, y <= M, a
+//                  negated base y is 4p - y (<= 4p, wide limbs)
+//   madd:  P = U2 - X1 + 4p <= 5.3, R = S2 - Y1 + 4p <= 5.3, RR, PP <= 1.17,
+//          X3 = reduce_q(RR - PPP - 2Q + 16p) <= 1.02, D = Q - X3 + 4p <= 5.3,
+//          Y3 = (R D + Y1 (4p - PPP)) / R' <= 1.21
+//   add:   the same with U1 for X1 and S1 for Y1
+//   dbl:   U = 2Y <= 8 (a wide base y in the doubling branch), V <= 1.39,
+//          M = 3X^2 <= 3.6, X3 reduced, Y3 = (M D + Y (4p - W)) / R' <= 1.21
+//   a stored Y never comes from a wide value unreduced (the first base of a
+//   bucket, a negation) -- rr_reduce_q takes it to <= 1.02.
 // Exceptional cases (P = 0 mod p: doubling or inverse) are detected on PP =
 // P^2, a product output, whose low limb screens them behind a branch that
 // waves almost never take.  The identity is the all-zero ZZ marker.
@@ -21,6 +39,11 @@
 #include "fieldrr.hpp"
 
 namespace ecg {
+
+template <class Q>
+constexpr bool rr_tight() {
+  return Q::SLACK_LOG2 < 16;
+}
 
 template <class Q>
 ECG_DEV bool xyzz_is_zero_rr(const XYZZ<FpR<Q>>& p) {
@@ -36,8 +59,13 @@ ECG_DEV void rr_dbl_core(const FpR<Q>& X, const FpR<Q>& Y, XYZZ<FpR<Q>>& r, FpR<
   rr_sqr2(U, X, V, X2);  // the two independent squarings as one interleaved pair
   rr_mul2(U, V, X, V, W, S);
   const F Mm = rr_add(rr_add(X2, X2), X2);
-  r.X = rr_sub2<16>(rr_sqr(Mm), S, S);
-  r.Y = rr_mul_sum2(Mm, rr_sub<64>(S, r.X), Y, rr_neg<4>(W));
+  if constexpr (rr_tight<Q>()) {
+    r.X = rr_reduce_q(rr_sub2<16>(rr_sqr(Mm), S, S));
+    r.Y = rr_mul_sum2(Mm, rr_sub<4>(S, r.X), Y, rr_neg<4>(W));
+  } else {
+    r.X = rr_sub2<16>(rr_sqr(Mm), S, S);
+    r.Y = rr_mul_sum2(Mm, rr_sub<64>(S, r.X), Y, rr_neg<4>(W));
+  }
 }
 
 // mdbl-2008-s-1: 2 (x, y)
@@ -85,21 +113,34 @@ ECG_DEV XYZZ<FpR<Q>> rr_add_affine(const XYZZ<FpR<Q>>& p, const Affine<FpR<Q>>& 
   XYZZ<F> r;
   // a.y (possibly wide) is carried only where it becomes a stored coordinate
   // (stored points are QN); the common path feeds it straight into a product
+  constexpr bool tight = rr_tight<Q>();
   if (xyzz_is_zero_rr(p)) {
     r.X = a.x;
     r.Y = rr_carry<Q>(a.y.v);
+    if constexpr (tight) r.Y = rr_reduce_q(r.Y);
     r.ZZ = F::one();
     r.ZZZ = F::one();
   } else {
     F U2, S2, PP, RR, PPP, Qv;
     rr_mul2(a.x, p.ZZ, a.y, p.ZZZ, U2, S2);
-    const F P = rr_sub<64>(U2, p.X);
-    const F R = rr_sub<16>(S2, p.Y);
+    F P, R;
+    if constexpr (tight) {
+      P = rr_sub<4>(U2, p.X);
+      R = rr_sub<4>(S2, p.Y);
+    } else {
+      P = rr_sub<64>(U2, p.X);
+      R = rr_sub<16>(S2, p.Y);
+    }
     rr_sqr2(P, R, PP, RR);
     rr_mul2(P, PP, p.X, PP, PPP, Qv);
     rr_mul2(p.ZZ, PP, p.ZZZ, PPP, r.ZZ, r.ZZZ);
-    r.X = rr_sub3<16>(RR, PPP, Qv, Qv);
-    r.Y = rr_mul_sum2(R, rr_sub<64>(Qv, r.X), p.Y, rr_neg<4>(PPP));
+    if constexpr (tight) {
+      r.X = rr_reduce_q(rr_sub3<16>(RR, PPP, Qv, Qv));
+      r.Y = rr_mul_sum2(R, rr_sub<4>(Qv, r.X), p.Y, rr_neg<4>(PPP));
+    } else {
+      r.X = rr_sub3<16>(RR, PPP, Qv, Qv);
+      r.Y = rr_mul_sum2(R, rr_sub<64>(Qv, r.X), p.Y, rr_neg<4>(PPP));
+    }
     if (rr_maybe_zero_prod(PP)) {  // rare: P = Q or P = -Q
       const bool inf = rr_is_zero_prod(PP);
       const bool dbl = inf && rr_is_zero_prod(RR);
@@ -135,8 +176,13 @@ ECG_DEV XYZZ<FpR<Q>> rr_add_xyzz(const XYZZ<FpR<Q>>& p, const XYZZ<FpR<Q>>& q) {
     rr_mul2(P, PP, U1, PP, PPP, Qv);
     rr_mul2(p.ZZ, q.ZZ, p.ZZZ, q.ZZZ, ZZ12, ZZZ12);
     rr_mul2(ZZ12, PP, ZZZ12, PPP, r.ZZ, r.ZZZ);
-    r.X = rr_sub3<16>(RR, PPP, Qv, Qv);
-    r.Y = rr_mul_sum2(R, rr_sub<64>(Qv, r.X), S1, rr_neg<4>(PPP));
+    if constexpr (rr_tight<Q>()) {
+      r.X = rr_reduce_q(rr_sub3<16>(RR, PPP, Qv, Qv));
+      r.Y = rr_mul_sum2(R, rr_sub<4>(Qv, r.X), S1, rr_neg<4>(PPP));
+    } else {
+      r.X = rr_sub3<16>(RR, PPP, Qv, Qv);
+      r.Y = rr_mul_sum2(R, rr_sub<64>(Qv, r.X), S1, rr_neg<4>(PPP));
+    }
     if (rr_maybe_zero_prod(PP)) {
       const bool inf = rr_is_zero_prod(PP);
       const bool dbl = inf && rr_is_zero_prod(RR);
@@ -198,7 +244,10 @@ ECG_DEV XYZZ<F> pa_neg(const XYZZ<F>& p) {
 template <class Q>
 ECG_DEV XYZZ<FpR<Q>> pa_neg(const XYZZ<FpR<Q>>& p) {
   XYZZ<FpR<Q>> r = p;
-  r.Y = rr_neg<8>(p.Y);
+  if constexpr (rr_tight<Q>())
+    r.Y = rr_reduce_q(rr_neg<4>(p.Y));
+  else
+    r.Y = rr_neg<8>(p.Y);
   return r;
 }
 
@@ -255,6 +304,16 @@ template <>
 struct RRof<params::bn254_fq> {
   using Q = params::bn254_fq_rr;
 };
+// G1 bucket layout: BN254 takes the 9 x 29-bit tight-slack form (fewer mads
+// per product); G2's Fq2 keeps RRof's 10 x 28 bits.
+template <class FqP>
+struct RR1of {
+  using Q = typename RRof<FqP>::Q;
+};
+template <>
+struct RR1of<params::bn254_fq> {
+  using Q = params::bn254_fq9_rr;
+};
 template <class C>
 constexpr bool has_rr_form() {
   return C::EXT == 1 && !std::is_same<typename RRof<typename C::FqParams>::Q, void>::value;
@@ -303,28 +362,39 @@ ECG_DEV XYZZ<Fp<typename Q::Base>> pa_to_std(const XYZZ<FpR<Q>>& p) {
 
 // ---------------------------------------------------------------------------
 // memory: a reduced-radix affine base is 2 NL words, an XYZZ point 4 NL words,
-// moved as 16-B vectors (NL even for both base-field layouts)
-// ---------------------------------------------------------------------------
+// moved as 16-B vectors.  A word count that is not a multiple of 4 (the 9-limb
+// BN254 G1 base: 18 words) moves whole vectors: the last one reads / writes
+// up to 3 words past the value, which the 128-B base records (BaseLayout)
+// leave as padding.
+template <int W>
+constexpr int rr_vec_words() {
+  return (W + 3) / 4 * 4;
+}
 template <class Q, int W>
 ECG_DEV void rr_load_words(const void* src, uint32_t* w) {
-  static_assert(W % 4 == 0, "16-B vector moves");
+  constexpr int V = rr_vec_words<W>();
   const uint4* s = reinterpret_cast<const uint4*>(src);
 #pragma unroll
-  for (int i = 0; i < W / 4; i++) {
+  for (int i = 0; i < V / 4; i++) {
     const uint4 t = s[i];
-    w[4 * i] = t.x;
-    w[4 * i + 1] = t.y;
-    w[4 * i + 2] = t.z;
-    w[4 * i + 3] = t.w;
+    const uint32_t q[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (4 * i + k < W) w[4 * i + k] = q[k];
   }
 }
 
 template <class Q, int W>
 ECG_DEV void rr_store_words(void* dst, const uint32_t* w) {
-  static_assert(W % 4 == 0, "16-B vector moves");
+  constexpr int V = rr_vec_words<W>();
   uint4* d = reinterpret_cast<uint4*>(dst);
 #pragma unroll
-  for (int i = 0; i < W / 4; i++) d[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+  for (int i = 0; i < V / 4; i++) {
+    uint32_t q[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) q[k] = 4 * i + k < W ? w[4 * i + k] : 0u;
+    d[i] = make_uint4(q[0], q[1], q[2], q[3]);
+  }
 }
 
 template <class Q>

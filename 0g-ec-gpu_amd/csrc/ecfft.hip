@@ -421,7 +421,7 @@ static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t lo
                    ecg_abort_cb abort_cb, void* user) {
   if constexpr (has_rr_form<C>()) {
     if (ecfft_rr_enabled())
-      return ecfft_pf<C, FpR<typename RRof<typename C::FqParams>::Q>>(ctx, d_jac, omega, log_n, s, abort_cb, user);
+      return ecfft_pf<C, FpR<typename RR1of<typename C::FqParams>::Q>>(ctx, d_jac, omega, log_n, s, abort_cb, user);
   }
   if constexpr (has_rr2_form<C>()) {
     if (ecfft_rr_enabled())

@@ -770,9 +770,10 @@ __global__ void __launch_bounds__(MSM_THREADS)
   store_affine(rec, r);
   // zero the record's pad too: whole-line writes (a partial line costs a
   // read-modify-write; measured 3.3 -> 5.6 ms for this kernel without it)
-  constexpr size_t pad = BaseLayout<AF>::BYTES - 2 * sizeof(AF);
+  constexpr size_t body = (2 * sizeof(AF) + 15) / 16 * 16;  // store_affine writes whole 16-B vectors
+  constexpr size_t pad = BaseLayout<AF>::BYTES - body;
   static_assert(pad % 16 == 0, "16-B vector stores");
-  uint4* tail = reinterpret_cast<uint4*>(reinterpret_cast<char*>(rec) + 2 * sizeof(AF));
+  uint4* tail = reinterpret_cast<uint4*>(reinterpret_cast<char*>(rec) + body);
 #pragma unroll
   for (size_t k = 0; k < pad / 16; k++) tail[k] = make_uint4(0, 0, 0, 0);
 }
@@ -814,7 +815,7 @@ template <class C>
 struct MsmField {
   using Q = typename RRof<typename C::FqParams>::Q;
   static constexpr bool rr = has_rr_form<C>() || has_rr2_form<C>();
-  using type = std::conditional_t<has_rr_form<C>(), FpR<Q>,
+  using type = std::conditional_t<has_rr_form<C>(), FpR<typename RR1of<typename C::FqParams>::Q>,
                                   std::conditional_t<has_rr2_form<C>(), FpR2<Q>, typename C::Fq>>;
 };
 
@@ -1306,7 +1307,7 @@ int msm_prepare_t(ecg_ctx* ctx, const void* d_bases, size_t n, uint32_t tab_c, v
   if constexpr (C::EXT == 1) {
     if constexpr (has_rr_form<C>()) {
       if (msm_rr_enabled())
-        return msm_table_rows_t<C, FpR<typename RRof<typename C::FqParams>::Q>>(d_bases, n, tab_c, d_out, s);
+        return msm_table_rows_t<C, FpR<typename RR1of<typename C::FqParams>::Q>>(d_bases, n, tab_c, d_out, s);
     }
     return msm_table_rows_t<C, typename C::Fq>(d_bases, n, tab_c, d_out, s);
   }

@@ -58,9 +58,10 @@ MSM_SEED = 0x35A00026
 NTT_SEED = 0x0FF70024
 KAT_A = 0x1234567890ABCDEF1122334455667788
 KAT_B = 0x0FEDCBA987654321
-# reduced-radix limbs of the MSM's Fq (fieldrr.hpp): 14 x 29 bits (BLS12-381), 10 x 28 (BN254)
-RR_LIMBS = {0: 14, 1: 10}
-RR_BITS = {0: 29, 1: 28}
+# reduced-radix limbs of the MSM's G1 Fq (fieldrr.hpp): 14 x 29 bits (BLS12-381), 9 x 29 (BN254,
+# the tight-slack layout bn254_fq9_rr)
+RR_LIMBS = {0: 14, 1: 9}
+RR_BITS = {0: 29, 1: 29}
 FR_RR_MADS = 2 * 9 * 9         # v_mad_u64_u32 per reduced-radix Fr product (9 x 29-bit limbs, ntt.hip)
 
 
