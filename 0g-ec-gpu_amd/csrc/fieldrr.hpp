@@ -84,22 +84,47 @@ ECG_DEV void mad64s(uint64_t& acc, uint32_t a, uint32_t b_uniform) {
 
 // Montgomery product (a b + m p) / R', product scanning, one v_mad_u64_u32
 // per product.
+// Moduli with P[0] = 1 (BLS12-381 Fr: r = 1 mod 2^32).  The digit m = -x mod
+// 2^B makes x + m the next multiple of 2^B, so the column carry is ceil(x /
+// 2^B) and the m P[0] mad is not needed.  The chains carry z = x - 1 instead
+// (column 0 starts at -1): ceil(x / 2^B) = (z >> B) + 1 with an arithmetic
+// shift, m = ~z mod 2^B, and the +1 of one column cancels the -1 of the next,
+// so only the last reduction column adds it back.  9 mads fewer per Fr
+// product; columns stay below 2^63 in magnitude, so z never wraps.
+template <class Q>
+constexpr bool rr_ceil_carry() {
+  return Q::P[0] == 1;
+}
+template <class Q>
+ECG_DEV void rr_ceil_step(uint64_t& z, uint32_t& m, bool last) {
+  constexpr uint32_t MASK = (1u << Q::BITS) - 1;
+  m = ~(uint32_t)z & MASK;
+  z = (uint64_t)((int64_t)z >> Q::BITS);
+  if (last) z += 1;
+}
+
+// Montgomery product (a b + m p) / R', product scanning, one v_mad_u64_u32
+// per product.
 template <class Q>
 ECG_DEV FpR<Q> rr_mul(const FpR<Q>& a, const FpR<Q>& b) {
   constexpr int NL = Q::NL, B = Q::BITS;
   constexpr uint32_t MASK = (1u << B) - 1;
   uint32_t m[NL];
   FpR<Q> r;
-  uint64_t acc = 0;
+  uint64_t acc = rr_ceil_carry<Q>() ? ~0ull : 0ull;
 #pragma unroll
   for (int k = 0; k < NL; k++) {
 #pragma unroll
     for (int i = 0; i <= k; i++) mad64(acc, a.v[i], b.v[k - i]);
 #pragma unroll
     for (int i = 0; i < k; i++) mad64s(acc, m[i], Q::P[k - i]);
-    m[k] = ((uint32_t)acc * Q::INV) & MASK;
-    mad64s(acc, m[k], Q::P[0]);  // low BITS bits of acc become 0
-    acc >>= B;
+    if constexpr (rr_ceil_carry<Q>()) {
+      rr_ceil_step<Q>(acc, m[k], k == NL - 1);
+    } else {
+      m[k] = ((uint32_t)acc * Q::INV) & MASK;
+      mad64s(acc, m[k], Q::P[0]);  // low BITS bits of acc become 0
+      acc >>= B;
+    }
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
@@ -208,6 +233,14 @@ ECG_DEV void mad64x2_z(uint64_t& acc0, uint32_t a0, uint32_t b0, uint64_t& acc1,
   else
     mad64x2(acc0, a0, b0, acc1, a1, b1);
 }
+// First products of both chains with an addend of -1 (rr_ceil_carry's z form).
+ECG_DEV void mad64x2_m1(uint64_t& acc0, uint32_t a0, uint32_t b0, uint64_t& acc1, uint32_t a1, uint32_t b1) {
+  uint64_t c0, c1;
+  asm("v_mad_u64_u32 %0, %2, %4, %5, -1\n\t"
+      "v_mad_u64_u32 %1, %3, %6, %7, -1"
+      : "=&v"(acc0), "=&v"(acc1), "=&s"(c0), "=&s"(c1)
+      : "v"(a0), "v"(b0), "v"(a1), "v"(b1));
+}
 // acc0 += a0 b0 + c0 d0; acc1 = a1 b1 + c1 d1 (chain 1 starts at zero)
 ECG_DEV void mad64x4_z1(uint64_t& acc0, uint32_t a0, uint32_t b0, uint32_t c0, uint32_t d0, uint64_t& acc1,
                         uint32_t a1, uint32_t b1, uint32_t c1, uint32_t d1) {
@@ -312,16 +345,24 @@ ECG_DEV void rr_mul2(const FpR<Q>& a0, const FpR<Q>& b0, const FpR<Q>& a1, const
   constexpr uint32_t MASK = (1u << B) - 1;
   uint32_t m0[NL], m1[NL];
   uint64_t x0, x1;
-  mad64x2_z<true, true>(x0, a0.v[0], b0.v[0], x1, a1.v[0], b1.v[0]);  // column 0 starts both chains
+  if constexpr (rr_ceil_carry<Q>())
+    mad64x2_m1(x0, a0.v[0], b0.v[0], x1, a1.v[0], b1.v[0]);  // column 0 starts both chains at -1
+  else
+    mad64x2_z<true, true>(x0, a0.v[0], b0.v[0], x1, a1.v[0], b1.v[0]);  // column 0 starts both chains
 #pragma unroll
   for (int k = 0; k < NL; k++) {
     if (k > 0) col2(k, 0, k, x0, a0.v, b0.v, x1, a1.v, b1.v);
     col2p<Q>(k, 0, k - 1, x0, m0, x1, m1);
-    m0[k] = ((uint32_t)x0 * Q::INV) & MASK;
-    m1[k] = ((uint32_t)x1 * Q::INV) & MASK;
-    mad64x2s(x0, m0[k], x1, m1[k], Q::P[0]);
-    x0 >>= B;
-    x1 >>= B;
+    if constexpr (rr_ceil_carry<Q>()) {
+      rr_ceil_step<Q>(x0, m0[k], k == NL - 1);
+      rr_ceil_step<Q>(x1, m1[k], k == NL - 1);
+    } else {
+      m0[k] = ((uint32_t)x0 * Q::INV) & MASK;
+      m1[k] = ((uint32_t)x1 * Q::INV) & MASK;
+      mad64x2s(x0, m0[k], x1, m1[k], Q::P[0]);
+      x0 >>= B;
+      x1 >>= B;
+    }
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {

@@ -337,7 +337,7 @@ template <class Q, int DEG, bool IN_RR, bool OUT_RR>
 __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_per_eu(ECG_NTT_RR_WAVES)))
     ntt_pass_rr_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, const uint4* __restrict__ pq_base,
                        uint32_t pq_cnt, uint32_t pq_shift, const uint4* __restrict__ twf_base, uint64_t twf_cnt,
-                       uint64_t twf_off, uint32_t log_n, uint32_t lgp, uint32_t log_g) {
+                       uint64_t twf_off, uint32_t log_n, uint32_t lgp, uint32_t log_g, uint32_t xcd_runs) {
   using F = FpR<Q>;
   constexpr uint32_t R = 1u << DEG;
   extern __shared__ uint4 smem[];
@@ -345,7 +345,12 @@ __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_pe
   const RrPlanes<Q> U = RrPlanes<Q>::over(smem, E);
   const uint32_t G = 1u << log_g;
   const size_t n = (size_t)1 << log_n;
-  const uint64_t g0 = (uint64_t)blockIdx.x << log_g;
+  // XCD-aware tile order (xcd_runs): blocks b and b + 8 share an XCD (round-robin
+  // dispatch), so XCD b % 8 takes a contiguous run of tiles.  Neighbouring tiles
+  // share the 128-B lines of the planes (4 columns of 16 + 16 + 4 B per tile
+  // row) and now meet in one L2 instead of fetching each line once per XCD.
+  const uint32_t tile = xcd_runs ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const uint64_t g0 = (uint64_t)tile << log_g;
   const RrPlanes<Q> PQ = RrPlanes<Q>::over(const_cast<uint4*>(pq_base), pq_cnt);
 
   // ---- load: u[i] = x[g + i t] * w^((n >> (lgp + DEG)) k i) (full per-pass table)
@@ -558,6 +563,14 @@ static hipError_t launch_pass(const PassArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+static bool ntt_xcd_runs() {  // XCD-aware tile order (A/B: ECG_NTT_XCD=0 keeps blockIdx order)
+  static bool v = [] {
+    const char* e = getenv("ECG_NTT_XCD");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // Tables of the reduced-radix passes (planes): pq (cnt entries) and the full
 // per-pass twiddles (twf_cnt entries over all passes, this pass at twf_off).
 struct RrTables {
@@ -588,7 +601,7 @@ static hipError_t launch_pass_rr(const PassArgs& a, const RrTables& t, hipStream
   }
   hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(threads), lds, s, (const uint4*)a.x, (uint4*)a.y,
                      (const uint4*)t.pq, t.pq_cnt, a.pq_shift, (const uint4*)t.twf, t.twf_cnt, t.twf_off, a.log_n,
-                     a.lgp, log_g);
+                     a.lgp, log_g, (uint32_t)(ntt_xcd_runs() && blocks >= 8 && blocks % 8 == 0));
   return hipGetLastError();
 }
 
