@@ -81,6 +81,10 @@ static uint32_t msm_combine_seg() {  // A/B: ECG_MSM_COMB_SEG
   }();
   return v;
 }
+static bool msm_short_runs() {  // A/B switch: ECG_MSM_SHORT=0 sends every record through the combine levels
+  static const bool v = env_u32("ECG_MSM_SHORT", 1) != 0;
+  return v;
+}
 static uint32_t msm_acc_seg() {  // sorted entries per accumulation thread
   static uint32_t v = env_u32("ECG_MSM_ACC_SEG", 128);
   return v;
@@ -531,6 +535,65 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
 }
 
 // ---------------------------------------------------------------------------
+// 4a. short record runs in one launch.  Every key's records are one contiguous
+//     run (2 per accumulation segment, in sorted order), and a bucket spans a
+//     few segments at most unless the scalars are skewed: with uniform digits
+//     the runs are 1-4 records long.  Thread t walks the runs that overlap its
+//     MSM_SHORT_SEG records: a run of <= MSM_SHORT_RUN records is summed by the
+//     thread whose window holds its first record (reading past its window if
+//     the run does) and stored as the bucket -- len - 1 full adds, where a
+//     combine level adds every record -- and its records' keys become KEY_END
+//     in kout, so the level-by-level combine below carries them as
+//     identities.  A longer run keeps its keys and raises *long_runs; with no
+//     long run every level returns at its first instruction.  Each thread
+//     writes kout for its own window only.  The 9-12 latency-bound levels (a
+//     chain of 8 full adds each) were 0.49 ms of a 2^20 MSM.
+// ---------------------------------------------------------------------------
+//     Latency pays for it below MSM_SHORT_MAX_RECS records (2^20 MSM: 4.44 ->
+//     4.05 ms; 2^23 at 2^21 records: no change); at 2^26 (13.6M records) the
+//     work is throughput-bound and this kernel's lanes idle beside the run
+//     owners (3.0 ms against 2.6 ms for all 12 levels,
+//     profiles/r03f/combine_short_ab.txt), so large MSMs keep the levels.
+constexpr uint32_t MSM_SHORT_RUN = 16;
+constexpr uint32_t MSM_SHORT_SEG = 4;
+constexpr size_t MSM_SHORT_MAX_RECS = (size_t)1 << 21;
+template <class F>
+__global__ void __launch_bounds__(MSM_THREADS)
+    msm_combine_short_kernel(const XYZZ<F>* __restrict__ rin, const uint32_t* __restrict__ kin, size_t n,
+                             uint32_t sentinel, XYZZ<F>* __restrict__ buckets, uint32_t* __restrict__ kout,
+                             uint32_t* __restrict__ long_runs) {
+  const size_t i0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * MSM_SHORT_SEG;
+  if (i0 >= n) return;
+  const size_t i1 = i0 + MSM_SHORT_SEG < n ? i0 + MSM_SHORT_SEG : n;
+  uint32_t k = kin[i0];
+  size_t s = i0;  // start of the run holding record i0 (searched MSM_SHORT_RUN + 1 back at most)
+  while (s > 0 && kin[s - 1] == k && i0 - s <= MSM_SHORT_RUN) s--;
+  bool raised = false;
+  for (size_t i = i0; i < i1;) {
+    size_t e = i + 1;  // one past the run's last record (searched until the run is known long)
+    while (e < n && kin[e] == k && e - s <= MSM_SHORT_RUN) e++;
+    const bool lng = e - s > MSM_SHORT_RUN;
+    const bool live = k < sentinel;  // KEY_END runs are identities
+    const size_t je = e < i1 ? e : i1;
+    for (size_t j = i; j < je; j++) kout[j] = live && !lng ? KEY_END : k;
+    if (live && lng) raised = true;
+    if (live && !lng && s >= i0) {  // this window holds the run's first record
+      XYZZ<F> acc = load_xyzz(&rin[s]);
+#pragma unroll 1
+      for (size_t j = s + 1; j < e; j++) acc = pa_add(acc, load_xyzz(&rin[j]));
+      store_xyzz(&buckets[k], acc);
+    }
+    if (lng) {  // skip to the run's end inside the window (its keys stay)
+      while (e < i1 && kin[e] == k) kout[e++] = k;
+    }
+    i = e;
+    s = e;
+    if (i < i1) k = kin[i];
+  }
+  if (raised) *long_runs = 1u;
+}
+
+// ---------------------------------------------------------------------------
 // 4. record combine: the same fixed-segment scheme over keyed partials
 //    (full XYZZ adds).  Interior runs are whole buckets; first/last runs go
 //    to the next level (2 per segment), so each level shrinks the record
@@ -543,10 +606,13 @@ template <class F>
 __global__ void __launch_bounds__(MSM_THREADS)
     msm_combine_kernel(const XYZZ<F>* __restrict__ rin, const uint32_t* __restrict__ kin, size_t n,
                        uint32_t sentinel, uint32_t seg, int final_level, XYZZ<F>* __restrict__ buckets,
-                       XYZZ<F>* __restrict__ rout, uint32_t* __restrict__ kout) {
+                       XYZZ<F>* __restrict__ rout, uint32_t* __restrict__ kout,
+                       const uint32_t* __restrict__ long_runs) {
   // Record keys are bucket indices or KEY_END (identity records of all-zero
-  // segments).  Runs of one key are contiguous; KEY_END runs may sit between
-  // blocks (window-padded mode), so they are carried along, never stored.
+  // segments, and the records msm_combine_short_kernel already summed).  Runs
+  // of one key are contiguous; KEY_END runs may sit between blocks
+  // (window-padded mode), so they are carried along, never stored.
+  if (long_runs && *long_runs == 0) return;  // every run was short: nothing left
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t e0 = t * seg;
   if (e0 >= n) return;
@@ -989,7 +1055,9 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   void *e0, *e1, *bk, *rc, *rk, *rc2, *rk2, *pa, *pb, *tmp;
   ECG_TRY(ws_get(ctx, "msm_e0", total * 8, &e0));
   ECG_TRY(ws_get(ctx, "msm_e1", total * 8, &e1));
-  ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nb * sizeof(X), &bk));
+  // the buckets, then one word: the long-run flag of msm_combine_short_kernel
+  ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nb * sizeof(X) + 256, &bk));
+  uint32_t* long_runs = (uint32_t*)((char*)bk + (size_t)nb * sizeof(X));
   ECG_TRY(ws_get(ctx, "msm_recs", 2 * nseg_all * sizeof(X), &rc));
   ECG_TRY(ws_get(ctx, "msm_rkeys", 2 * nseg_all * 4, &rk));
   const uint32_t comb_seg = msm_combine_seg();
@@ -1003,7 +1071,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   // buckets nobody writes (no term) stay the identity: all-zero XYZZ (ZZ = 0).
   // (Running this clear and the base conversion on a side stream, concurrent
   // with the digits and the sorts, measured no gain: all are HBM-bound.)
-  ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X), s));
+  ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X) + 4, s));
   const F* bases = (const F*)d_bases;
   if constexpr (!std::is_same<F, typename C::Fq>::value) {
     const size_t nb_in = (size_t)g.n_lines * g.line_len;  // every base a value can index
@@ -1056,18 +1124,30 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   ECG_HIP(hipGetLastError());
   ECG_TRY(kt_end(ctx, "msm_accumulate", s));
 
-  // combine the segment-edge partials, level by level
+  // combine the segment-edge partials: the short runs in one launch, then
+  // what is left level by level
   size_t nrec = 2 * nseg_all;
   X* rin = (X*)rc;
   uint32_t* kin = (uint32_t*)rk;
   X* rout = (X*)rc2;
   uint32_t* kout = (uint32_t*)rk2;
+  const uint32_t* lflag = nullptr;
+  if (msm_short_runs() && nrec < MSM_SHORT_MAX_RECS) {
+    void* ks;
+    ECG_TRY(ws_get(ctx, "msm_rkeys_short", nrec * 4, &ks));
+    hipLaunchKernelGGL(msm_combine_short_kernel<F>,
+                       dim3(blocks_for((nrec + MSM_SHORT_SEG - 1) / MSM_SHORT_SEG, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                       (const X*)rin, (const uint32_t*)kin, nrec, sentinel, (X*)bk, (uint32_t*)ks, long_runs);
+    ECG_HIP(hipGetLastError());
+    kin = (uint32_t*)ks;
+    lflag = long_runs;
+  }
   for (;;) {
     const bool fin = nrec <= comb_seg;
     const size_t nthr = (nrec + comb_seg - 1) / comb_seg;
     hipLaunchKernelGGL(msm_combine_kernel<F>, dim3(blocks_for(nthr, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
                        (const X*)rin, (const uint32_t*)kin, nrec, sentinel, comb_seg, fin ? 1 : 0, (X*)bk,
-                       rout, kout);
+                       rout, kout, lflag);
     ECG_HIP(hipGetLastError());
     if (fin) break;
     nrec = 2 * nthr;
