@@ -41,6 +41,34 @@ __global__ void check_kv(const uint64_t* k, size_t n, unsigned* bad) {
   if (i + 1 < n && (k[i] >> 32) > (k[i + 1] >> 32)) atomicAdd(bad, 1u);
 }
 
+// 6-byte entries: 20-bit key in the low bits (w[0] + low 4 bits of w[1]),
+// 28 value bits above -- 6 B instead of 8 B moved per entry and pass.
+struct K6 {
+  uint16_t w[3];
+};
+struct K6Dec {
+  __host__ __device__ rocprim::tuple<uint16_t&, uint16_t&, uint16_t&> operator()(K6& k) const {
+    return rocprim::tuple<uint16_t&, uint16_t&, uint16_t&>(k.w[2], k.w[1], k.w[0]);
+  }
+};
+__global__ void gen6(const uint64_t* kv, K6* k6, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t key = (uint32_t)(kv[i] >> 32), val = (uint32_t)kv[i] & 0x0fffffffu;
+  K6 e;
+  e.w[0] = (uint16_t)key;
+  e.w[1] = (uint16_t)((key >> 16) | ((val & 0xfffu) << 4));
+  e.w[2] = (uint16_t)(val >> 12);
+  k6[i] = e;
+}
+__global__ void check_k6(const K6* k, size_t n, unsigned* bad) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i + 1 >= n) return;
+  const uint32_t a = k[i].w[0] | ((uint32_t)(k[i].w[1] & 15) << 16);
+  const uint32_t b = k[i + 1].w[0] | ((uint32_t)(k[i + 1].w[1] & 15) << 16);
+  if (a > b) atomicAdd(bad, 1u);
+}
+
 struct Bufs {
   uint32_t *k0, *k1, *v0, *v1;
   uint64_t *kv0, *kv1;
@@ -99,6 +127,30 @@ void run_kv(const char* name, Bufs& b, hipStream_t s) {
   printf("%-40s best %.3f ms avg %.3f ms  %.2f TB/s  %s\n", name, best, sum / (reps - 1), gb / best, bad ? "UNSORTED" : "ok");
 }
 
+template <class C>
+void run_k6(const char* name, Bufs& b, K6* a, K6* o, hipStream_t s) {
+  size_t bytes = 0;
+  CHK(rocprim::radix_sort_keys<C>(nullptr, bytes, a, o, b.n, K6Dec{}, 0, 20, s));
+  if (bytes > b.tmp_bytes) { printf("%-40s tmp %zu too big\n", name, bytes); return; }
+  hipEvent_t e0, e1;
+  CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
+  float best = 1e9, sum = 0;
+  const int reps = 7;
+  for (int r = 0; r < reps; r++) {
+    CHK(hipEventRecord(e0, s));
+    CHK(rocprim::radix_sort_keys<C>(b.tmp, bytes, a, o, b.n, K6Dec{}, 0, 20, s));
+    CHK(hipEventRecord(e1, s));
+    CHK(hipEventSynchronize(e1));
+    float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
+    if (r > 0) { best = ms < best ? ms : best; sum += ms; }
+  }
+  CHK(hipMemsetAsync(b.bad, 0, 4, s));
+  check_k6<<<(b.n + 255) / 256, 256, 0, s>>>(o, b.n, b.bad);
+  unsigned bad; CHK(hipMemcpy(&bad, b.bad, 4, hipMemcpyDeviceToHost));
+  const double gb = 2.0 * 12.0 * b.n / 1e9 + 6.0 * b.n / 1e9;
+  printf("%-40s best %.3f ms avg %.3f ms  %.2f TB/s  %s\n", name, best, sum / (reps - 1), gb / best, bad ? "UNSORTED" : "ok");
+}
+
 int main(int argc, char** argv) {
   const int logn = argc > 1 ? atoi(argv[1]) : 26;
   Bufs b;
@@ -124,6 +176,19 @@ int main(int argc, char** argv) {
   run_pairs<Cfg<1024, 16, 10, A::match>>("pairs 1024x16 r10 match", b, s);
   run_pairs<Cfg<1024, 12, 11, A::match>>("pairs 1024x12 r11 match", b, s);
   run_pairs<Cfg<1024, 12, 8, A::match>>("pairs 1024x12 r8 match (3 passes)", b, s);
+  if (argc > 2) {  // 6-byte entries only (plus the current u64 form for reference)
+    K6 *a6, *o6;
+    CHK(hipMalloc(&a6, b.n * 6)); CHK(hipMalloc(&o6, b.n * 6));
+    gen6<<<(b.n + 255) / 256, 256, 0, s>>>(b.kv0, a6, b.n);
+    CHK(hipStreamSynchronize(s));
+    run_kv<Cfg<1024, 12, 10, A::match>>("u64 keys 1024x12 r10 match (current)", b, s);
+    run_k6<Cfg<1024, 12, 10, A::match>>("K6 keys 1024x12 r10 match", b, a6, o6, s);
+    run_k6<Cfg<1024, 16, 10, A::match>>("K6 keys 1024x16 r10 match", b, a6, o6, s);
+    run_k6<Cfg<1024, 8, 10, A::match>>("K6 keys 1024x8 r10 match", b, a6, o6, s);
+    run_k6<Cfg<512, 16, 10, A::match>>("K6 keys 512x16 r10 match", b, a6, o6, s);
+    run_k6<rocprim::default_config>("K6 keys default", b, a6, o6, s);
+    return 0;
+  }
   run_kv<Cfg<1024, 12, 10, A::match>>("u64 keys 1024x12 r10 match", b, s);
   run_kv<Cfg<512, 16, 10, A::match>>("u64 keys 512x16 r10 match", b, s);
   run_kv<Cfg<1024, 8, 10, A::match>>("u64 keys 1024x8 r10 match", b, s);
