@@ -364,6 +364,29 @@ def test_msm_skewed_scalars_2p22(gpu_programs, pattern):
 
 
 @pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_record_runs_around_short_threshold(gpu_programs, cname, cid):
+    """Groups of equal scalars whose buckets hold 900-3000 terms in every
+    window: 7-24 accumulation segments, i.e. record runs on both sides of
+    msm_combine_short_kernel's 16-record limit (short runs summed in its one
+    launch, long ones left to the combine levels), beside uniform scalars in
+    1-4-record runs.  Checked by the KAT at 2^16 (below 2^21 records, where
+    the short pass runs)."""
+    cv = po.CURVES[cname]
+    prog = gpu_programs[0][0]
+    n = 1 << 16
+    a, b = 0x5A5A17, 0x2B2B29
+    E = rand_scalars_np(cv, n, 1616 + cid)
+    pos = 0
+    for g, size in enumerate((900, 1000, 1016, 1024, 1040, 1088, 1100, 1200, 3000)):
+        E[pos:pos + size] = rand_scalars_np(cv, 1, 7000 + g)[0]
+        pos += size
+    d_b = ecgpu.gen_bases_dev(prog, cname, a, b, n)
+    out = ecgpu.msm_dev(prog, cname, d_b, ecgpu.DeviceBuffer.upload(prog, E), n)
+    assert normalised_form_ok(cid, out)
+    assert same_point(cid, out, co.gen_mul(cid, co.kat_scalar(cid, a, b, E, nthreads=16)))
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
 def test_msm_equal_and_opposite_bases(gpu_programs, cname, cid):
     """Every base equal (mixed-add and full-add doublings in every bucket,
     record and reduction level) and a base beside its negative with equal
