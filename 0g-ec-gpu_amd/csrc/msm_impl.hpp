@@ -773,8 +773,14 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
     if (j0 + k < cnt) acc = pa_add(acc, load_xyzz(&src[j0 + k]));
   pts.put(t, acc);
   __syncthreads();
+  // only as many LDS levels as this workgroup has inputs for (a second launch
+  // over a few workgroup sums ran all 8 levels: 2^20, 8 sums per window)
+  const uint32_t left = cnt - b * MSM_THREADS * MSM_TREE_K;
+  const uint32_t active = left >= MSM_THREADS * MSM_TREE_K ? MSM_THREADS : (left + MSM_TREE_K - 1) / MSM_TREE_K;
+  uint32_t top = 1;
+  while (top < active) top <<= 1;
 #pragma unroll 1
-  for (uint32_t stride = MSM_THREADS / 2; stride > 0; stride >>= 1) {
+  for (uint32_t stride = top / 2; stride > 0; stride >>= 1) {
     if (t < stride) pts.put(t, pa_add(pts.get(t), pts.get(t + stride)));
     __syncthreads();
   }
