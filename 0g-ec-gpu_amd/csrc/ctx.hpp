@@ -119,8 +119,9 @@ inline hipStream_t pick_stream(ecg_ctx* ctx, void* s) {
 
 // Engine entry points (ntt.hip / msm.hip); data pointers are device memory.
 int ntt_validate(int field_id, uint32_t log_n);
+// batch: that many same-size transforms with the same omega, back to back at d_data
 int ntt_run(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uint32_t log_n,
-            hipStream_t s, ecg_abort_cb abort_cb, void* user);
+            hipStream_t s, ecg_abort_cb abort_cb, void* user, uint32_t batch = 1);
 // MSM / point-sum results are written to HOST memory (3 x Lq u64, normalised
 // Jacobian): the last serial steps (window fold, normalisation) run on the host.
 // scalar_mont: scalars are Montgomery Fr elements (converted on device).

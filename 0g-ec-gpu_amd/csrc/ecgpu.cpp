@@ -267,6 +267,37 @@ int ecg_fft(ecg_ctx* ctx, int field_id, uint64_t* inout, const uint64_t* omega, 
   return kt_collect(ctx);
 }
 
+// Same-size transforms with the same omega, back to back in one device buffer
+// and run as ONE batched transform (each pass launches every transform's
+// tiles together): a 2^16 transform alone is 64 workgroups on 256 CUs.
+// Results are identical to one ecg_fft per input.
+constexpr size_t FFT_BATCH_BYTES = (size_t)1 << 30;
+static int fft_batch(ecg_ctx* ctx, int field_id, uint64_t** inouts, const uint64_t* omega, uint32_t log_n,
+                     size_t cnt, ecg_abort_cb abort_cb, void* user) {
+  ECG_ENTER(ctx);
+  ECG_TRY(ntt_validate(field_id, log_n));
+  const size_t bytes = ((size_t)1 << log_n) * fr_bytes(field_id);
+  void* d;
+  ECG_TRY(ws_get(ctx, "fft_io", cnt * bytes, &d));
+  hipStream_t s = ctx->stream;
+  for (size_t b = 0; b < cnt; b++) {
+    if (!inouts[b]) {
+      set_error("ecg_fft_many: null pointer");
+      return ECG_ERR_INVALID;
+    }
+    ECG_HIP(hipMemcpyAsync((uint8_t*)d + b * bytes, inouts[b], bytes, hipMemcpyHostToDevice, s));  // fft.rs:89
+  }
+  int rc = ntt_run(ctx, field_id, d, omega, log_n, s, abort_cb, user, (uint32_t)cnt);
+  if (rc != ECG_OK) {
+    (void)hipStreamSynchronize(s);
+    return rc;
+  }
+  for (size_t b = 0; b < cnt; b++)
+    ECG_HIP(hipMemcpyAsync(inouts[b], (uint8_t*)d + b * bytes, bytes, hipMemcpyDeviceToHost, s));  // fft.rs:129
+  ECG_HIP(hipStreamSynchronize(s));
+  return kt_collect(ctx);
+}
+
 int ecg_fft_many(ecg_ctx** ctxs, int nctx, int field_id, uint64_t** inouts, const uint64_t* omegas,
                  const uint32_t* log_ns, size_t count, ecg_abort_cb abort_cb, void* user) {
   if (!ctxs || nctx <= 0) {
@@ -282,9 +313,16 @@ int ecg_fft_many(ecg_ctx** ctxs, int nctx, int field_id, uint64_t** inouts, cons
   for (int d = 0; d < nctx && (size_t)d * chunk < count; d++) {
     th.emplace_back([&, d]() {
       const size_t i0 = d * chunk, i1 = std::min(count, i0 + chunk);
-      for (size_t i = i0; i < i1; i++) {
+      for (size_t i = i0, j; i < i1; i = j) {
         if (first_err.load() != ECG_OK) break;  // fft.rs:233-235
-        int rc = ecg_fft(ctxs[d], field_id, inouts[i], omegas + 4 * i, log_ns[i], abort_cb, user);
+        // the run of inputs sharing this one's size and omega (fft_batch)
+        const size_t one = ((size_t)1 << std::min(log_ns[i], 40u)) * fr_bytes(field_id);
+        j = i + 1;
+        while (j < i1 && log_ns[j] == log_ns[i] && memcmp(omegas + 4 * j, omegas + 4 * i, 32) == 0 &&
+               (j - i + 1) * one <= FFT_BATCH_BYTES)
+          j++;
+        int rc = j - i == 1 ? ecg_fft(ctxs[d], field_id, inouts[i], omegas + 4 * i, log_ns[i], abort_cb, user)
+                            : fft_batch(ctxs[d], field_id, inouts + i, omegas + 4 * i, log_ns[i], j - i, abort_cb, user);
         if (rc != ECG_OK) {
           int expected = ECG_OK;
           if (first_err.compare_exchange_strong(expected, rc)) {

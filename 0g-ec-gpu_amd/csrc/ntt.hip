@@ -337,7 +337,8 @@ template <class Q, int DEG, bool IN_RR, bool OUT_RR>
 __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_per_eu(ECG_NTT_RR_WAVES)))
     ntt_pass_rr_kernel(const uint4* __restrict__ x, uint4* __restrict__ y, const uint4* __restrict__ pq_base,
                        uint32_t pq_cnt, uint32_t pq_shift, const uint4* __restrict__ twf_base, uint64_t twf_cnt,
-                       uint64_t twf_off, uint32_t log_n, uint32_t lgp, uint32_t log_g, uint32_t xcd_runs) {
+                       uint64_t twf_off, uint32_t log_n, uint32_t lgp, uint32_t log_g, uint32_t xcd_runs,
+                       uint32_t log_tiles) {
   using F = FpR<Q>;
   constexpr uint32_t R = 1u << DEG;
   extern __shared__ uint4 smem[];
@@ -349,7 +350,13 @@ __global__ void __launch_bounds__(NTT_RR_THREADS) __attribute__((amdgpu_waves_pe
   // dispatch), so XCD b % 8 takes a contiguous run of tiles.  Neighbouring tiles
   // share the 128-B lines of the planes (4 columns of 16 + 16 + 4 B per tile
   // row) and now meet in one L2 instead of fetching each line once per XCD.
-  const uint32_t tile = xcd_runs ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  const uint32_t tile_all = xcd_runs ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3) : blockIdx.x;
+  // batched transforms (radix_fft_many): transform tile_all >> log_tiles of the
+  // batch, stored back to back in the input's and the output's layout
+  const uint32_t tile = tile_all & ((1u << log_tiles) - 1);
+  const size_t tix = tile_all >> log_tiles;
+  x += tix * (IN_RR ? ((size_t)9 << log_n) / 4 : (size_t)2 << log_n);  // 36 B or 32 B per element, in uint4
+  y += tix * (OUT_RR ? ((size_t)9 << log_n) / 4 : (size_t)2 << log_n);
   const uint64_t g0 = (uint64_t)tile << log_g;
   const RrPlanes<Q> PQ = RrPlanes<Q>::over(const_cast<uint4*>(pq_base), pq_cnt);
 
@@ -523,6 +530,7 @@ struct PassArgs {
   const void* tw_hi;
   const void* twf;  // full table of this pass, or null
   uint32_t log_n, lgp;
+  uint32_t batch = 1;  // transforms back to back (reduced-radix passes only)
 };
 
 // A/B knob: log2 elements per workgroup (ECG_NTT_TILE, default 10)
@@ -599,9 +607,12 @@ static hipError_t launch_pass_rr(const PassArgs& a, const RrTables& t, hipStream
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(threads), lds, s, (const uint4*)a.x, (uint4*)a.y,
+  const uint64_t grid = blocks * a.batch;
+  uint32_t log_tiles = 0;
+  while ((1ull << log_tiles) < blocks) log_tiles++;
+  hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(threads), lds, s, (const uint4*)a.x, (uint4*)a.y,
                      (const uint4*)t.pq, t.pq_cnt, a.pq_shift, (const uint4*)t.twf, t.twf_cnt, t.twf_off, a.log_n,
-                     a.lgp, log_g, (uint32_t)(ntt_xcd_runs() && blocks >= 8 && blocks % 8 == 0));
+                     a.lgp, log_g, (uint32_t)(ntt_xcd_runs() && grid >= 8 && grid % 8 == 0), log_tiles);
   return hipGetLastError();
 }
 
@@ -703,7 +714,7 @@ static int plan_passes(uint32_t log_n, int variant, uint32_t* degs) {
 
 template <class P, class Q>
 static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uint32_t log_n,
-                     hipStream_t s, ecg_abort_cb abort_cb, void* user) {
+                     hipStream_t s, ecg_abort_cb abort_cb, void* user, uint32_t batch = 1) {
   using F = Fp<P>;
   const int variant = ntt_variant();
   uint32_t degs[40];
@@ -723,13 +734,18 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
   // bytes per element between passes: the plane layout for the reduced-radix
   // passes, the boundary layout otherwise
   const size_t elem = rr ? RR_PLANE_BYTES : sizeof(F);
+  if (batch > 1 && !rr) {  // batched launches are a reduced-radix feature: one transform at a time
+    for (uint32_t b = 0; b < batch; b++)
+      ECG_TRY((ntt_run_t<P, Q>(ctx, field_id, (F*)d_data + b * n, omega, log_n, s, abort_cb, user, 1)));
+    return ECG_OK;
+  }
 
   void *scratch = nullptr, *scratch2 = nullptr, *tables;
-  if (np > 1 || variant == 1) ECG_TRY(ws_get(ctx, "ntt_scratch", n * elem, &scratch));
+  if (np > 1 || variant == 1) ECG_TRY(ws_get(ctx, "ntt_scratch", batch * n * elem, &scratch));
   // odd pass counts (> 1) rotate through a second scratch buffer so the last
   // pass writes d_data directly (no copy back; HBM is plentiful); the
   // reduced-radix inner passes always rotate two (planes do not fit d_data)
-  if (np > 1 && ((np & 1) || (rr && np > 2))) ECG_TRY(ws_get(ctx, "ntt_scratch2", n * elem, &scratch2));
+  if (np > 1 && ((np & 1) || (rr && np > 2))) ECG_TRY(ws_get(ctx, "ntt_scratch2", batch * n * elem, &scratch2));
   ECG_TRY(ws_get(ctx, "ntt_tables", (pq_cnt + lo_cnt + hi_cnt) * sizeof(F), &tables));
   F* pq = (F*)tables;
   F* tw_lo = pq + pq_cnt;
@@ -813,7 +829,7 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
   uint32_t lgp = 0;
   for (int k = 0; k < np; k++) {
     if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // fft.rs:94-98
-    const PassArgs a{bufs[k], bufs[k + 1], pq, max_deg - degs[k], tw_lo, tw_hi, twf[k], log_n, lgp};
+    const PassArgs a{bufs[k], bufs[k + 1], pq, max_deg - degs[k], tw_lo, tw_hi, twf[k], log_n, lgp, batch};
     ECG_TRY(kt_begin(ctx, "ntt_pass", s));
     hipError_t e;
     if (rr) {
@@ -826,7 +842,8 @@ static int ntt_run_t(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* o
     ECG_TRY(kt_end(ctx, "ntt_pass", s));
     lgp += degs[k];
   }
-  if (bufs[np] != d_data) ECG_HIP(hipMemcpyAsync(d_data, bufs[np], n * sizeof(F), hipMemcpyDeviceToDevice, s));
+  if (bufs[np] != d_data)
+    ECG_HIP(hipMemcpyAsync(d_data, bufs[np], batch * n * sizeof(F), hipMemcpyDeviceToDevice, s));
   return ECG_OK;
 }
 
@@ -851,15 +868,16 @@ int ntt_validate(int field_id, uint32_t log_n) {
 }
 
 int ntt_run(ecg_ctx* ctx, int field_id, void* d_data, const uint64_t* omega, uint32_t log_n, hipStream_t s,
-            ecg_abort_cb abort_cb, void* user) {
+            ecg_abort_cb abort_cb, void* user, uint32_t batch) {
   ECG_TRY(ntt_validate(field_id, log_n));
+  if (batch == 0) return ECG_OK;
   switch (field_id) {
     case ECG_FIELD_BLS12_381_FR:
       return ntt_run_t<params::bls12_381_fr, params::bls12_381_fr_rr>(ctx, field_id, d_data, omega, log_n, s,
-                                                                       abort_cb, user);
+                                                                       abort_cb, user, batch);
     default:
       return ntt_run_t<params::bn254_fr, params::bn254_fr_rr>(ctx, field_id, d_data, omega, log_n, s, abort_cb,
-                                                               user);
+                                                               user, batch);
   }
 }
 
