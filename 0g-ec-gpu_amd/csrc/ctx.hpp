@@ -136,7 +136,7 @@ int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count
                   hipStream_t s);
 int ecfft_validate(int curve_id, uint32_t log_n);
 int ecfft_run(ecg_ctx* ctx, int curve_id, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
-              ecg_abort_cb abort_cb, void* user);
+              ecg_abort_cb abort_cb, void* user, uint32_t batch = 1);
 // distributed NTT (dfft.hip) and RCCL exchange (comm.cpp)
 int dfft_stage1(int field_id, const void* d_in, void* d_out, const uint64_t* omega, uint32_t T, uint32_t rank,
                 uint32_t log_n, hipStream_t s);

@@ -60,16 +60,20 @@ ECG_DEV XYZZ<PF> to_pf(const XYZZ<typename C::Fq>& p) {
 
 template <class C, class PF>
 __global__ void __launch_bounds__(ECFFT_THREADS)
-    ecfft_load_kernel(const typename C::Fq* __restrict__ jac, uint32_t log_n, XYZZ<PF>* __restrict__ a) {
+    ecfft_load_kernel(const typename C::Fq* __restrict__ jac, uint32_t log_n, uint32_t batch,
+                      XYZZ<PF>* __restrict__ a) {
+  // batch transforms back to back (radix_ec_fft_many runs): point i of the
+  // batch is point i mod n of transform i >> log_n
   using F = typename C::Fq;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (1u << log_n)) return;
+  if (i >= (batch << log_n)) return;
   Jac<F> j;
   j.X = load(&jac[3 * (size_t)i]);
   j.Y = load(&jac[3 * (size_t)i + 1]);
   j.Z = load(&jac[3 * (size_t)i + 2]);
-  const uint32_t r = log_n ? (__brev(i) >> (32 - log_n)) : 0u;
-  store_xyzz(&a[r], to_pf<C, PF>(xyzz_from_jac(j)));
+  const uint32_t il = i & ((1u << log_n) - 1);
+  const uint32_t r = log_n ? (__brev(il) >> (32 - log_n)) : 0u;
+  store_xyzz(&a[(i - il) + r], to_pf<C, PF>(xyzz_from_jac(j)));
 }
 
 template <class C>
@@ -296,12 +300,15 @@ ECG_DEV XYZZ<PF> win_mul(const XYZZ<PF>& P, const uint32_t* k, XYZZ<PF>* __restr
 template <class C, class PF>
 __global__ void __launch_bounds__(ECFFT_THREADS)
     ecfft_stage_win_kernel(XYZZ<PF>* __restrict__ a, const uint4* __restrict__ tw, uint32_t log_n, uint32_t s,
-                           XYZZ<PF>* __restrict__ tabs) {
+                           uint32_t batch, XYZZ<PF>* __restrict__ tabs) {
   constexpr bool glv = has_glv<C>();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t t = glv ? g >> 1 : g;
-  const uint32_t half = glv ? (g & 1) : 0u;
-  if (t >= (1u << (log_n - 1))) return;  // both lanes of a pair leave together
+  const uint32_t lanes_log = glv ? log_n : log_n - 1;  // lanes per transform (2 per butterfly on GLV curves)
+  if (g >= (batch << lanes_log)) return;               // both lanes of a pair leave together
+  a += (size_t)(g >> lanes_log) << log_n;              // transform g >> lanes_log of the batch
+  const uint32_t gl = g & ((1u << lanes_log) - 1);
+  const uint32_t t = glv ? gl >> 1 : gl;
+  const uint32_t half = glv ? (gl & 1) : 0u;
   const uint32_t h = 1u << s;
   const uint32_t j = t & (h - 1);
   const uint32_t i0 = ((t >> s) << (s + 1)) + j, i1 = i0 + h;
@@ -367,25 +374,31 @@ static bool ecfft_rr_enabled() {  // A/B switch: ECG_ECFFT_RR=0 keeps the 32-bit
 
 template <class C, class PF>
 static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
-                    ecg_abort_cb abort_cb, void* user) {
+                    ecg_abort_cb abort_cb, void* user, uint32_t batch) {
   using F = typename C::Fq;
   using S = Fp<typename C::FrParams>;
   const uint32_t n = 1u << log_n;
-  void *a, *tw, *gt = nullptr;
-  ECG_TRY(ws_get(ctx, "ecfft_pts", (size_t)n * sizeof(XYZZ<PF>), &a));
-  ECG_TRY(ws_get(ctx, "ecfft_tw", (size_t)(n / 2 + 1) * 32, &tw));
   // windowed stages for the reduced-radix point forms (the 32-bit-limb forms
   // are the A/B baseline and keep the bit ladders)
   const bool win = !std::is_same<PF, F>::value && ecfft_win_enabled();
-  const size_t lanes = has_glv<C>() && win ? n : n / 2 + 1;  // stage lanes (2 per butterfly on GLV curves)
+  if (batch > 1 && (!win || log_n == 0)) {  // batched stages are a windowed-form feature
+    for (uint32_t b = 0; b < batch; b++)
+      ECG_TRY((ecfft_pf<C, PF>(ctx, (F*)d_jac + 3 * (size_t)b * n, omega, log_n, s, abort_cb, user, 1)));
+    return ECG_OK;
+  }
+  const size_t nb = (size_t)batch * n;
+  void *a, *tw, *gt = nullptr;
+  ECG_TRY(ws_get(ctx, "ecfft_pts", nb * sizeof(XYZZ<PF>), &a));
+  ECG_TRY(ws_get(ctx, "ecfft_tw", (size_t)(n / 2 + 1) * 32, &tw));
+  const size_t lanes = has_glv<C>() && win ? nb : (size_t)batch * (n / 2) + 1;  // stage lanes (2 per butterfly on GLV curves)
   if (win)
     ECG_TRY(ws_get(ctx, "ecfft_tab", lanes * ECFFT_TAB * sizeof(XYZZ<PF>), &gt));
   else if (has_glv<C>())
     ECG_TRY(ws_get(ctx, "ecfft_glv", (size_t)(n / 2 + 1) * 3 * sizeof(XYZZ<PF>), &gt));
   S om;
   memcpy(om.v, omega, sizeof(om.v));
-  hipLaunchKernelGGL((ecfft_load_kernel<C, PF>), dim3(ecfft_blocks(n)), dim3(ECFFT_THREADS), 0, s, (const F*)d_jac, log_n,
-                     (XYZZ<PF>*)a);
+  hipLaunchKernelGGL((ecfft_load_kernel<C, PF>), dim3(ecfft_blocks(nb)), dim3(ECFFT_THREADS), 0, s, (const F*)d_jac,
+                     log_n, batch, (XYZZ<PF>*)a);
   ECG_HIP(hipGetLastError());
   if (log_n > 0) {
     hipLaunchKernelGGL(ecfft_twiddle_kernel<C>, dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s, om, n / 2,
@@ -401,8 +414,9 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
     ECG_TRY(kt_begin(ctx, "ecfft_stage", s));
     if constexpr (!std::is_same<PF, F>::value) {
       if (win)
-        hipLaunchKernelGGL((ecfft_stage_win_kernel<C, PF>), dim3(ecfft_blocks(has_glv<C>() ? n : n / 2)),
-                           dim3(ECFFT_THREADS), 0, s, (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, (XYZZ<PF>*)gt);
+        hipLaunchKernelGGL((ecfft_stage_win_kernel<C, PF>), dim3(ecfft_blocks(has_glv<C>() ? nb : nb / 2)),
+                           dim3(ECFFT_THREADS), 0, s, (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, batch,
+                           (XYZZ<PF>*)gt);
     }
     if (!win)
       hipLaunchKernelGGL((ecfft_stage_kernel<C, PF>), dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s,
@@ -410,24 +424,26 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
     ECG_HIP(hipGetLastError());
     ECG_TRY(kt_end(ctx, "ecfft_stage", s));
   }
-  hipLaunchKernelGGL((ecfft_store_kernel<C, PF>), dim3(ecfft_blocks(n)), dim3(ECFFT_THREADS), 0, s, (const XYZZ<PF>*)a, n,
-                     (F*)d_jac);
+  hipLaunchKernelGGL((ecfft_store_kernel<C, PF>), dim3(ecfft_blocks(nb)), dim3(ECFFT_THREADS), 0, s,
+                     (const XYZZ<PF>*)a, (uint32_t)nb, (F*)d_jac);
   ECG_HIP(hipGetLastError());
   return ECG_OK;
 }
 
 template <class C>
 static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
-                   ecg_abort_cb abort_cb, void* user) {
+                   ecg_abort_cb abort_cb, void* user, uint32_t batch) {
   if constexpr (has_rr_form<C>()) {
     if (ecfft_rr_enabled())
-      return ecfft_pf<C, FpR<typename RR1of<typename C::FqParams>::Q>>(ctx, d_jac, omega, log_n, s, abort_cb, user);
+      return ecfft_pf<C, FpR<typename RR1of<typename C::FqParams>::Q>>(ctx, d_jac, omega, log_n, s, abort_cb, user,
+                                                                         batch);
   }
   if constexpr (has_rr2_form<C>()) {
     if (ecfft_rr_enabled())
-      return ecfft_pf<C, FpR2<typename RRof<typename C::FqParams>::Q>>(ctx, d_jac, omega, log_n, s, abort_cb, user);
+      return ecfft_pf<C, FpR2<typename RRof<typename C::FqParams>::Q>>(ctx, d_jac, omega, log_n, s, abort_cb, user,
+                                                                         batch);
   }
-  return ecfft_pf<C, typename C::Fq>(ctx, d_jac, omega, log_n, s, abort_cb, user);
+  return ecfft_pf<C, typename C::Fq>(ctx, d_jac, omega, log_n, s, abort_cb, user, batch);
 }
 
 int ecfft_validate(int curve_id, uint32_t log_n) {
@@ -445,10 +461,11 @@ int ecfft_validate(int curve_id, uint32_t log_n) {
 }
 
 int ecfft_run(ecg_ctx* ctx, int curve_id, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
-              ecg_abort_cb abort_cb, void* user) {
+              ecg_abort_cb abort_cb, void* user, uint32_t batch) {
   ECG_TRY(ecfft_validate(curve_id, log_n));
+  if (batch == 0) return ECG_OK;
   return with_curve(curve_id, "ec_fft",
-                    [&](auto c) { return ecfft_t<decltype(c)>(ctx, d_jac, omega, log_n, s, abort_cb, user); });
+                    [&](auto c) { return ecfft_t<decltype(c)>(ctx, d_jac, omega, log_n, s, abort_cb, user, batch); });
 }
 
 }  // namespace ecg

@@ -376,6 +376,36 @@ int ecg_ec_fft_dev(ecg_ctx* ctx, int curve_id, void* d_inout_jac, const uint64_t
   return kt_collect(ctx);
 }
 
+// Same-size EC-FFTs with the same omega, back to back and run as ONE batched
+// transform (every stage launches the whole run's butterflies): the small
+// transforms 0g runs are latency-bound at under one wave per SIMD each.
+constexpr size_t ECFFT_BATCH_POINTS = (size_t)1 << 20;
+static int ec_fft_batch(ecg_ctx* ctx, int curve_id, uint64_t** inouts, const uint64_t* omega, uint32_t log_n,
+                        size_t cnt, ecg_abort_cb abort_cb, void* user) {
+  ECG_ENTER(ctx);
+  ECG_TRY(ecfft_validate(curve_id, log_n));
+  const size_t bytes = ((size_t)1 << log_n) * 3 * fq_limbs64(curve_id) * 8;
+  void* d;
+  ECG_TRY(ws_get(ctx, "ecfft_io", cnt * bytes, &d));
+  hipStream_t s = ctx->stream;
+  for (size_t b = 0; b < cnt; b++) {
+    if (!inouts[b]) {
+      set_error("ecg_ec_fft_many: null pointer");
+      return ECG_ERR_INVALID;
+    }
+    ECG_HIP(hipMemcpyAsync((uint8_t*)d + b * bytes, inouts[b], bytes, hipMemcpyHostToDevice, s));  // ec_fft.rs:103
+  }
+  int rc = ecfft_run(ctx, curve_id, d, omega, log_n, s, abort_cb, user, (uint32_t)cnt);
+  if (rc != ECG_OK) {
+    (void)hipStreamSynchronize(s);
+    return rc;
+  }
+  for (size_t b = 0; b < cnt; b++)
+    ECG_HIP(hipMemcpyAsync(inouts[b], (uint8_t*)d + b * bytes, bytes, hipMemcpyDeviceToHost, s));  // ec_fft.rs:158
+  ECG_HIP(hipStreamSynchronize(s));
+  return kt_collect(ctx);
+}
+
 int ecg_ec_fft_many(ecg_ctx** ctxs, int nctx, int curve_id, uint64_t** inouts, const uint64_t* omegas,
                     const uint32_t* log_ns, size_t count, ecg_abort_cb abort_cb, void* user) {
   if (!ctxs || nctx <= 0) {
@@ -391,9 +421,17 @@ int ecg_ec_fft_many(ecg_ctx** ctxs, int nctx, int curve_id, uint64_t** inouts, c
   for (int d = 0; d < nctx && (size_t)d * chunk < count; d++) {
     th.emplace_back([&, d]() {
       const size_t i0 = d * chunk, i1 = std::min(count, i0 + chunk);
-      for (size_t i = i0; i < i1; i++) {
+      for (size_t i = i0, j; i < i1; i = j) {
         if (first_err.load() != ECG_OK) break;  // ec_fft.rs:249-251
-        int rc = ecg_ec_fft(ctxs[d], curve_id, inouts[i], omegas + 4 * i, log_ns[i], abort_cb, user);
+        // the run of inputs sharing this one's size and omega (ec_fft_batch)
+        const size_t one = (size_t)1 << std::min(log_ns[i], 40u);
+        j = i + 1;
+        while (j < i1 && log_ns[j] == log_ns[i] && memcmp(omegas + 4 * j, omegas + 4 * i, 32) == 0 &&
+               (j - i + 1) * one <= ECFFT_BATCH_POINTS)
+          j++;
+        int rc = j - i == 1
+                     ? ecg_ec_fft(ctxs[d], curve_id, inouts[i], omegas + 4 * i, log_ns[i], abort_cb, user)
+                     : ec_fft_batch(ctxs[d], curve_id, inouts + i, omegas + 4 * i, log_ns[i], j - i, abort_cb, user);
         if (rc != ECG_OK) {
           int expected = ECG_OK;
           if (first_err.compare_exchange_strong(expected, rc)) {

@@ -166,6 +166,30 @@ def test_ec_fft_many_three_contexts(progs):
 
 
 @pytest.mark.parametrize("cname,cid", CURVES)
+def test_ec_fft_many_batched_runs(progs, cname, cid):
+    """Runs of same-size, same-omega EC-FFT inputs as one batched transform
+    (ecgpu.cpp ec_fft_batch: every stage launches the whole run's butterflies,
+    two GLV lanes each on BLS12-381): runs of 5 at 2^8, 3 at 2^6 with the
+    inverse omega in the middle (the run splits), a single 2^7 and a pair of
+    2^9, each against serial_ec_fft."""
+    cv = po.CURVES[cname]
+    f, lq = cv.fr, cv.fq.limbs64
+    one = co.u64arr([cv.fq.to_mont(1)], lq)[0]
+    log_ns = [8] * 5 + [6] * 3 + [7] + [9, 9]
+    ins, oms = [], []
+    for i, ln in enumerate(log_ns):
+        aff = co.gen_bases(cid, 77 + i, 13, 1 << ln, 4)
+        ins.append(np.ascontiguousarray(np.concatenate([aff, np.tile(one, (1 << ln, 1))], axis=1)))
+        w = f.omega(1 << ln)
+        oms.append(co.u64arr([f.to_mont(pow(w, -1, f.modulus) if i == 6 else w)], 4)[0])
+    want = [co.serial_ec_fft(cid, a.copy(), om, ln) for a, om, ln in zip(ins, oms, log_ns)]
+    ecgpu.EcFftKernel.create(progs[:1], cname).radix_ec_fft_many(ins, oms, log_ns)
+    for k, (a, w) in enumerate(zip(ins, want)):
+        for p, q in zip(a, w):
+            assert same(cid, p, q), k
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
 def test_msm_pass_size_from_memory(progs, cname, cid):
     """calc_chunk_size analogue: sized from the 288 GB of HBM, a 2^26-term MSM
     is one pass; at most 2^31 - 1 terms per pass."""
