@@ -501,6 +501,24 @@ def main():
         aux["ec_fft"] = {"log_n": le, "ms": ef_s * 1e3, "butterflies_per_s": (1 << (le - 1)) * le / ef_s}
         d_jac.free()
         d_pts.free()
+        # radix_ec_fft_many over 16 same-size inputs (the 2^16 points cut into 2^12
+        # slices): one batched transform, beside one radix_ec_fft call per input
+        lm, cm = 12, 16
+        ek = ecgpu.EcFftKernel.create([prog], args.curve)
+        om_m = omega_for(cid, r_int, lm)
+        xs = [np.ascontiguousarray(jac[i << lm:(i + 1) << lm]) for i in range(cm)]
+        ys = [x.copy() for x in xs]
+        t_a = time.perf_counter()
+        ek.radix_ec_fft_many(xs, [om_m] * cm, [lm] * cm)
+        em_s = time.perf_counter() - t_a
+        t_a = time.perf_counter()
+        for y in ys:
+            ek.radix_ec_fft(y, om_m, lm)
+        e1_s = time.perf_counter() - t_a
+        aux["ec_fft_many"] = {"log_n": lm, "count": cm, "ms": em_s * 1e3, "ms_one_call_per_input": e1_s * 1e3,
+                              "equal": all(bool((x == y).all()) for x, y in zip(xs, ys)),
+                              "note": "host buffers in and out (EcFftKernel::radix_ec_fft_many); the run of "
+                                      "equal-size, equal-omega inputs is one batched transform"}
         # G2 MSM over Fq2: 2^22 terms, prepared bases, KAT-checked
         g2 = args.curve + "_g2"
         lg = 22
