@@ -379,7 +379,13 @@ int ecg_ec_fft_dev(ecg_ctx* ctx, int curve_id, void* d_inout_jac, const uint64_t
 // Same-size EC-FFTs with the same omega, back to back and run as ONE batched
 // transform (every stage launches the whole run's butterflies): the small
 // transforms 0g runs are latency-bound at under one wave per SIMD each.
-constexpr size_t ECFFT_BATCH_POINTS = (size_t)1 << 20;
+static size_t ecfft_batch_points() {  // points per batched run (A/B: ECG_ECFFT_BATCH_LOG)
+  static const size_t v = [] {
+    const char* e = getenv("ECG_ECFFT_BATCH_LOG");
+    return (size_t)1 << (e ? atoi(e) : 20);
+  }();
+  return v;
+}
 static int ec_fft_batch(ecg_ctx* ctx, int curve_id, uint64_t** inouts, const uint64_t* omega, uint32_t log_n,
                         size_t cnt, ecg_abort_cb abort_cb, void* user) {
   ECG_ENTER(ctx);
@@ -427,7 +433,7 @@ int ecg_ec_fft_many(ecg_ctx** ctxs, int nctx, int curve_id, uint64_t** inouts, c
         const size_t one = (size_t)1 << std::min(log_ns[i], 40u);
         j = i + 1;
         while (j < i1 && log_ns[j] == log_ns[i] && memcmp(omegas + 4 * j, omegas + 4 * i, 32) == 0 &&
-               (j - i + 1) * one <= ECFFT_BATCH_POINTS)
+               (j - i + 1) * one <= ecfft_batch_points())
           j++;
         int rc = j - i == 1
                      ? ecg_ec_fft(ctxs[d], curve_id, inouts[i], omegas + 4 * i, log_ns[i], abort_cb, user)
