@@ -5,61 +5,225 @@
 // per-device partial points.  Here each rank owns one MI355X and one ecg_ctx;
 // RCCL (linked from /opt/rocm, the same HIP runtime as the rest of the
 // library) moves device buffers directly:
-//   * MSM: ncclAllGather of the per-rank Jacobian partial (3 x Lq u64),
+//   * MSM: ncclAllGather of the per-rank [status | Jacobian partial] record,
 //     then the EC fold (RCCL has no EC-add reduction);
-//   * one NTT split over ranks: three equal-split ncclAllToAll (dfft.hip).
+//   * one NTT split over ranks: three equal-split ncclAllToAll (dfft.hip),
+//     with status exchanges before the first and the last.
 // Rendezvous: the 128-byte ncclUniqueId travels through the caller's
 // launcher (ecgpu.dist.HostGroup in bench.py: one authenticated local socket
 // per rank, no torch in the process).
+//
+// Failure semantics.  The reference stops every device at the first error
+// (first-writer-wins result, multiexp.rs:345-365, fft.rs:218-245).  Across
+// processes the equivalent is that no rank may leave its peers inside a
+// collective: every distributed call exchanges each rank's status before its
+// payload collectives (comm_agree, or the status word of the MSM record), so
+// a local failure becomes the same error on every rank.  What a status
+// exchange cannot cover -- a peer that crashed, or a device fault mid-flight
+// -- is bounded by a deadline: the communicator is non-blocking, every call
+// and every wait polls ncclCommGetAsyncError against it, and on expiry the
+// communicator is aborted (ncclCommAbort) and the call returns an error.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "ctx.hpp"
 
 namespace ecg {
 
-#define ECG_NCCL(call)                                                                             \
-  do {                                                                                             \
-    ncclResult_t r_ = (call);                                                                      \
-    if (r_ != ncclSuccess) {                                                                       \
-      ::ecg::set_error("RCCL error %s at %s:%d", ncclGetErrorString(r_), __FILE__, __LINE__);      \
-      return ECG_ERR_RCCL;                                                                         \
-    }                                                                                              \
-  } while (0)
+namespace {
 
-int comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes_per_peer, hipStream_t s) {
-  if (ctx->comm_size > 1 && !ctx->comm) {
-    set_error("comm_alltoall: %d ranks but no communicator", ctx->comm_size);
+constexpr uint32_t DEFAULT_TIMEOUT_MS = 300000;
+
+uint32_t comm_timeout(const ecg_ctx* ctx) {
+  if (ctx->comm_timeout_ms) return ctx->comm_timeout_ms;
+  const char* e = getenv("ECG_COMM_TIMEOUT_S");
+  const long v = e ? atol(e) : 0;
+  return v > 0 && v < 4000000 ? (uint32_t)(v * 1000) : DEFAULT_TIMEOUT_MS;
+}
+
+using Clock = std::chrono::steady_clock;
+
+struct Deadline {
+  Clock::time_point end;
+  int polls = 0;
+  explicit Deadline(uint32_t ms) : end(Clock::now() + std::chrono::milliseconds(ms)) {}
+  bool expired() const { return Clock::now() >= end; }
+  // spin briefly (small collectives finish in tens of us), then back off
+  void pause() {
+    if (++polls < 200)
+      std::this_thread::yield();
+    else
+      std::this_thread::sleep_for(std::chrono::microseconds(polls < 2000 ? 20 : 200));
+  }
+};
+
+bool host_transport(const ecg_ctx* ctx) { return ctx->xchg != nullptr; }
+
+// Abort the RCCL communicator after a failure or a timeout: its kernels stop,
+// later distributed calls are refused (comm_size > 1, no communicator).
+void comm_abort(ecg_ctx* ctx) {
+  if (ctx->comm) (void)ncclCommAbort((ncclComm_t)ctx->comm);
+  ctx->comm = nullptr;
+}
+
+int rccl_fail(ecg_ctx* ctx, ncclResult_t r, const char* what) {
+  set_error("%s: RCCL error %s (%s); communicator aborted", what, ncclGetErrorString(r),
+            ncclGetLastError((ncclComm_t)ctx->comm));
+  comm_abort(ctx);
+  return ECG_ERR_RCCL;
+}
+
+// A call on a non-blocking communicator returns ncclInProgress while it is
+// still being set up (connections to peers are made lazily): poll its state
+// until it settles, under the deadline.
+int rccl_settle(ecg_ctx* ctx, ncclResult_t r, const char* what) {
+  Deadline dl(comm_timeout(ctx));
+  while (r == ncclInProgress) {
+    if (dl.expired()) {
+      set_error("%s: RCCL call still in progress after %u ms (a peer rank failed or never arrived); "
+                "communicator aborted", what, comm_timeout(ctx));
+      comm_abort(ctx);
+      return ECG_ERR_RCCL;
+    }
+    dl.pause();
+    if (ncclCommGetAsyncError((ncclComm_t)ctx->comm, &r) != ncclSuccess) r = ncclSystemError;
+  }
+  return r == ncclSuccess ? ECG_OK : rccl_fail(ctx, r, what);
+}
+
+int need_comm(ecg_ctx* ctx, const char* what) {
+  if (ctx->comm_size > 1 && !ctx->comm && !ctx->xchg) {
+    set_error("%s: %d ranks but no communicator (never initialised, or aborted after a failure)", what,
+              ctx->comm_size);
     return ECG_ERR_RCCL;
   }
-  if (ctx->comm_size == 1) {  // one rank: the exchange is a copy
+  return ECG_OK;
+}
+
+// Host transport: stage through host memory, the caller's callback moves it.
+int host_exchange(ecg_ctx* ctx, int op, const void* d_send, void* d_recv, size_t bytes, hipStream_t s,
+                  const char* what) {
+  const size_t P = (size_t)ctx->comm_size;
+  std::vector<uint8_t> send(op == ECG_XCHG_ALLGATHER ? bytes : bytes * P), recv(bytes * P);
+  if (!send.empty()) ECG_HIP(hipMemcpyAsync(send.data(), d_send, send.size(), hipMemcpyDeviceToHost, s));
+  ECG_HIP(hipStreamSynchronize(s));
+  if (ctx->xchg(op, send.data(), recv.data(), bytes, ctx->xchg_user) != 0) {
+    set_error("%s: the host transport failed", what);
+    return ECG_ERR_RCCL;
+  }
+  if (!recv.empty()) ECG_HIP(hipMemcpyAsync(d_recv, recv.data(), recv.size(), hipMemcpyHostToDevice, s));
+  ECG_HIP(hipStreamSynchronize(s));
+  return ECG_OK;
+}
+
+}  // namespace
+
+#define ECG_NCCL(ctx, call, what)                                    \
+  do {                                                               \
+    ncclResult_t r_ = (call);                                        \
+    if (r_ != ncclSuccess) ECG_TRY(rccl_settle((ctx), r_, (what)));  \
+  } while (0)
+
+int comm_wait(ecg_ctx* ctx, hipStream_t s, const char* what) {
+  if (!ctx->comm) {  // no RCCL work can be pending: a plain wait
+    ECG_HIP(hipStreamSynchronize(s));
+    return ECG_OK;
+  }
+  Deadline dl(comm_timeout(ctx));
+  for (;;) {
+    hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return ECG_OK;
+    if (e != hipErrorNotReady) {
+      set_error("%s: HIP error %s while waiting for the exchange; communicator aborted", what, hipGetErrorName(e));
+      comm_abort(ctx);
+      return ECG_ERR_HIP;
+    }
+    ncclResult_t ae = ncclSuccess;
+    if (ncclCommGetAsyncError((ncclComm_t)ctx->comm, &ae) != ncclSuccess) ae = ncclSystemError;
+    if (ae != ncclSuccess && ae != ncclInProgress) return rccl_fail(ctx, ae, what);
+    if (dl.expired()) {
+      set_error("%s: no progress within %u ms (a peer rank failed or never arrived); communicator aborted", what,
+                comm_timeout(ctx));
+      comm_abort(ctx);
+      return ECG_ERR_RCCL;
+    }
+    dl.pause();
+  }
+}
+
+int comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes_per_peer, hipStream_t s) {
+  ECG_TRY(need_comm(ctx, "alltoall"));
+  if (host_transport(ctx)) return host_exchange(ctx, ECG_XCHG_ALLTOALL, d_send, d_recv, bytes_per_peer, s, "alltoall");
+  if (!ctx->comm) {  // one rank: the exchange is a copy
     ECG_HIP(hipMemcpyAsync(d_recv, d_send, bytes_per_peer * ctx->comm_size, hipMemcpyDeviceToDevice, s));
     return ECG_OK;
   }
-  ECG_NCCL(ncclAllToAll(d_send, d_recv, bytes_per_peer, ncclUint8, (ncclComm_t)ctx->comm, s));
+  ECG_NCCL(ctx, ncclAllToAll(d_send, d_recv, bytes_per_peer, ncclUint8, (ncclComm_t)ctx->comm, s), "alltoall");
+  return ECG_OK;
+}
+
+int comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes, hipStream_t s) {
+  ECG_TRY(need_comm(ctx, "allgather"));
+  if (host_transport(ctx)) return host_exchange(ctx, ECG_XCHG_ALLGATHER, d_send, d_recv, bytes, s, "allgather");
+  if (!ctx->comm) {
+    ECG_HIP(hipMemcpyAsync(d_recv, d_send, bytes, hipMemcpyDeviceToDevice, s));
+    return ECG_OK;
+  }
+  ECG_NCCL(ctx, ncclAllGather(d_send, d_recv, bytes, ncclUint8, (ncclComm_t)ctx->comm, s), "allgather");
   return ECG_OK;
 }
 
 void comm_free(ecg_ctx* ctx) {
   if (ctx->comm) (void)ncclCommDestroy((ncclComm_t)ctx->comm);
   ctx->comm = nullptr;
+  ctx->xchg = nullptr;
+  ctx->xchg_user = nullptr;
   ctx->comm_size = 1;
   ctx->comm_rank = 0;
 }
 
-int comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes, hipStream_t s) {
-  if (ctx->comm_size > 1 && !ctx->comm) {
-    set_error("comm_allgather: %d ranks but no communicator", ctx->comm_size);
-    return ECG_ERR_RCCL;
+// Status words ride in fixed-size records so ranks that disagree on the
+// call's arguments still exchange equal byte counts.
+constexpr int AGREE_WORDS = 4;
+
+int comm_agree(ecg_ctx* ctx, int local_rc, const uint64_t* agree, int n_agree, const char* what, hipStream_t s) {
+  const int P = ctx->comm_size;
+  if (P == 1 && !ctx->comm) return local_rc;
+  ECG_TRY(need_comm(ctx, what));
+  const std::string local_msg = local_rc != ECG_OK ? last_error_text() : "";
+  uint64_t rec[1 + AGREE_WORDS] = {(uint64_t)(int64_t)local_rc, 0, 0, 0, 0};
+  for (int i = 0; i < n_agree && i < AGREE_WORDS; i++) rec[1 + i] = agree[i];
+  void *d_rec, *d_all;
+  ECG_TRY(ws_get(ctx, "comm_agree", sizeof rec, &d_rec));
+  ECG_TRY(ws_get(ctx, "comm_agree_all", sizeof rec * P, &d_all));
+  std::vector<uint64_t> all((1 + AGREE_WORDS) * (size_t)P);
+  ECG_HIP(hipMemcpyAsync(d_rec, rec, sizeof rec, hipMemcpyHostToDevice, s));
+  ECG_TRY(comm_allgather(ctx, d_rec, d_all, sizeof rec, s));
+  ECG_TRY(comm_wait(ctx, s, what));
+  ECG_HIP(hipMemcpyAsync(all.data(), d_all, sizeof rec * P, hipMemcpyDeviceToHost, s));
+  ECG_HIP(hipStreamSynchronize(s));
+  for (int r = 0; r < P; r++) {
+    const int rc = (int)(int64_t)all[(size_t)r * (1 + AGREE_WORDS)];
+    if (rc == ECG_OK) continue;
+    if (r == ctx->comm_rank)
+      set_error("%s", local_msg.c_str());
+    else
+      set_error("%s: rank %d of %d failed (rc=%d); every rank stops", what, r, P, rc);
+    return rc;
   }
-  if (ctx->comm_size == 1) {
-    ECG_HIP(hipMemcpyAsync(d_recv, d_send, bytes, hipMemcpyDeviceToDevice, s));
-    return ECG_OK;
-  }
-  ECG_NCCL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, (ncclComm_t)ctx->comm, s));
+  for (int r = 0; r < P; r++)
+    if (memcmp(&all[(size_t)r * (1 + AGREE_WORDS) + 1], &rec[1], AGREE_WORDS * 8) != 0) {
+      set_error("%s: rank %d was called with other arguments than rank %d (field / curve / size differ)", what, r,
+                ctx->comm_rank);
+      return ECG_ERR_INVALID;
+    }
   return ECG_OK;
 }
 
@@ -75,8 +239,18 @@ int ecg_comm_unique_id(uint8_t* out) {
     return ECG_ERR_INVALID;
   }
   ncclUniqueId id;
-  ECG_NCCL(ncclGetUniqueId(&id));
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    set_error("ncclGetUniqueId: %s", ncclGetErrorString(r));
+    return ECG_ERR_RCCL;
+  }
   memcpy(out, id.internal, NCCL_UNIQUE_ID_BYTES);
+  return ECG_OK;
+}
+
+int ecg_comm_set_timeout(ecg_ctx* ctx, uint32_t ms) {
+  ECG_ENTER(ctx);
+  ctx->comm_timeout_ms = ms;
   return ECG_OK;
 }
 
@@ -86,20 +260,49 @@ int ecg_comm_init(ecg_ctx* ctx, int nranks, int rank, const uint8_t* unique_id) 
     set_error("ecg_comm_init: bad arguments (nranks %d, rank %d)", nranks, rank);
     return ECG_ERR_INVALID;
   }
+  (void)hipStreamSynchronize(ctx->stream);
   comm_free(ctx);  // back to the single-rank state until the new communicator exists
-  if (nranks == 1) return ECG_OK;
+  if (!unique_id) return ECG_OK;  // one rank, no communicator
   ncclUniqueId id;
   memcpy(id.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
-  ncclComm_t c;
-  ECG_NCCL(ncclCommInitRank(&c, nranks, id, rank));
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;  // every wait below runs under the deadline
+  ncclComm_t c = nullptr;
+  ncclResult_t r = ncclCommInitRankConfig(&c, nranks, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    set_error("ncclCommInitRankConfig: %s", ncclGetErrorString(r));
+    if (c) (void)ncclCommAbort(c);
+    return ECG_ERR_RCCL;
+  }
   ctx->comm = c;
+  ctx->comm_size = nranks;
+  ctx->comm_rank = rank;
+  int rc = rccl_settle(ctx, r, "ecg_comm_init");
+  if (rc != ECG_OK) {
+    ctx->comm_size = 1;  // nothing to refuse: the caller re-initialises
+    ctx->comm_rank = 0;
+  }
+  return rc;
+}
+
+int ecg_comm_init_host(ecg_ctx* ctx, int nranks, int rank, ecg_xchg_cb xchg, void* user) {
+  ECG_ENTER(ctx);
+  if (nranks < 1 || rank < 0 || rank >= nranks || !xchg) {
+    set_error("ecg_comm_init_host: bad arguments (nranks %d, rank %d, callback %p)", nranks, rank, (void*)xchg);
+    return ECG_ERR_INVALID;
+  }
+  (void)hipStreamSynchronize(ctx->stream);
+  comm_free(ctx);
+  ctx->xchg = xchg;
+  ctx->xchg_user = user;
   ctx->comm_size = nranks;
   ctx->comm_rank = rank;
   return ECG_OK;
 }
 
 void ecg_comm_destroy(ecg_ctx* ctx) {
-  if (!ctx || !ctx->comm) return;
+  if (!ctx) return;
+  std::lock_guard<std::recursive_mutex> g(ctx->mu);
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   comm_free(ctx);
@@ -108,57 +311,95 @@ void ecg_comm_destroy(ecg_ctx* ctx) {
 int ecg_comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes) {
   ECG_ENTER(ctx);
   ECG_TRY(comm_allgather(ctx, d_send, d_recv, bytes, ctx->stream));
-  ECG_HIP(hipStreamSynchronize(ctx->stream));
-  return ECG_OK;
+  return comm_wait(ctx, ctx->stream, "ecg_comm_allgather");
 }
 
 int ecg_comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes_per_peer) {
   ECG_ENTER(ctx);
   ECG_TRY(comm_alltoall(ctx, d_send, d_recv, bytes_per_peer, ctx->stream));
-  ECG_HIP(hipStreamSynchronize(ctx->stream));
-  return ECG_OK;
+  return comm_wait(ctx, ctx->stream, "ecg_comm_alltoall");
 }
 
-// MSM over this rank's shard; the per-rank partials are all-gathered over
-// RCCL and folded, so every rank returns the full result.
-int ecg_msm_dist(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n_local,
-                 uint64_t* out_jac) {
+// MSM over this rank's shard; the per-rank [status | curve | partial] records
+// are all-gathered and, when every rank succeeded, the partials folded, so
+// every rank returns the full result -- or the same error.
+int ecg_msm_dist_ex(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n_local,
+                    uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
   ECG_ENTER(ctx);
+  hipStream_t s = ctx->stream;
+  constexpr size_t PW = 3 * (size_t)ECG_MAX_COORD_U64;  // partial words, the largest curve's
+  uint64_t rec[2 + PW] = {};
+  int rc = ECG_OK;
   if (!out_jac || ((!d_bases || !d_scalars) && n_local)) {
     set_error("ecg_msm_dist: null pointer");
-    return ECG_ERR_INVALID;
-  }
-  if (!curve_valid(curve_id)) {
+    rc = ECG_ERR_INVALID;
+  } else if (!curve_valid(curve_id)) {
     set_error("multiexp: unknown curve_id %d", curve_id);
-    return ECG_ERR_INVALID;
+    rc = ECG_ERR_INVALID;
+  } else if (abort_cb && abort_cb(user)) {
+    rc = ECG_ABORTED;
+  } else {
+    rc = msm_run(ctx, curve_id, d_bases, d_scalars, n_local, rec + 2, s, abort_cb, user);
   }
-  hipStream_t s = ctx->stream;
-  const size_t pb = 3 * (size_t)fq_limbs64(curve_id) * 8;
-  uint64_t part[3 * ECG_MAX_COORD_U64];
-  ECG_TRY(msm_run(ctx, curve_id, d_bases, d_scalars, n_local, part, s, nullptr, nullptr));
-  void *d_part, *d_all;
-  ECG_TRY(ws_get(ctx, "dist_part", pb, &d_part));
-  ECG_TRY(ws_get(ctx, "dist_all", pb * ctx->comm_size, &d_all));
-  ECG_HIP(hipMemcpyAsync(d_part, part, pb, hipMemcpyHostToDevice, s));
-  ECG_TRY(comm_allgather(ctx, d_part, d_all, pb, s));
-  std::vector<uint64_t> all(pb / 8 * ctx->comm_size);
-  ECG_HIP(hipMemcpyAsync(all.data(), d_all, pb * ctx->comm_size, hipMemcpyDeviceToHost, s));
+  if (ctx->comm_size == 1 && !ctx->comm) {  // one rank: the partial is the result
+    if (rc != ECG_OK) return rc;
+    memcpy(out_jac, rec + 2, 3 * (size_t)fq_limbs64(curve_id) * 8);
+    return kt_collect(ctx);
+  }
+  const std::string local_msg = rc != ECG_OK ? last_error_text() : "";
+  if (rc != ECG_OK) (void)hipStreamSynchronize(s);  // the failed run's work is done or abandoned
+  rec[0] = (uint64_t)(int64_t)rc;
+  rec[1] = (uint64_t)(uint32_t)curve_id;
+  const int P = ctx->comm_size;
+  void *d_rec, *d_all;
+  ECG_TRY(ws_get(ctx, "dist_rec", sizeof rec, &d_rec));
+  ECG_TRY(ws_get(ctx, "dist_all", sizeof rec * P, &d_all));
+  ECG_HIP(hipMemcpyAsync(d_rec, rec, sizeof rec, hipMemcpyHostToDevice, s));
+  ECG_TRY(comm_allgather(ctx, d_rec, d_all, sizeof rec, s));
+  ECG_TRY(comm_wait(ctx, s, "ecg_msm_dist"));
+  std::vector<uint64_t> all((2 + PW) * (size_t)P);
+  ECG_HIP(hipMemcpyAsync(all.data(), d_all, sizeof rec * P, hipMemcpyDeviceToHost, s));
   ECG_HIP(hipStreamSynchronize(s));
-  ECG_TRY(point_sum_host(curve_id, all.data(), ctx->comm_size, out_jac));  // multiexp.rs:394-397
+  for (int r = 0; r < P; r++) {  // the lowest failing rank's code, on every rank
+    const int rrc = (int)(int64_t)all[(size_t)r * (2 + PW)];
+    if (rrc == ECG_OK) continue;
+    if (r == ctx->comm_rank)
+      set_error("%s", local_msg.c_str());
+    else
+      set_error("ecg_msm_dist: rank %d of %d failed (rc=%d); every rank stops", r, P, rrc);
+    return rrc;
+  }
+  const size_t pw = 3 * (size_t)fq_limbs64(curve_id);
+  std::vector<uint64_t> parts(pw * P);
+  for (int r = 0; r < P; r++) {
+    if ((int)all[(size_t)r * (2 + PW) + 1] != curve_id) {
+      set_error("ecg_msm_dist: rank %d ran curve %d, this rank curve %d", r, (int)all[(size_t)r * (2 + PW) + 1],
+                curve_id);
+      return ECG_ERR_INVALID;
+    }
+    memcpy(&parts[pw * r], &all[(size_t)r * (2 + PW) + 2], pw * 8);
+  }
+  ECG_TRY(point_sum_host(curve_id, parts.data(), (size_t)P, out_jac));  // multiexp.rs:394-397
   return kt_collect(ctx);
+}
+
+int ecg_msm_dist(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n_local,
+                 uint64_t* out_jac) {
+  return ecg_msm_dist_ex(ctx, curve_id, d_bases, d_scalars, n_local, out_jac, nullptr, nullptr);
 }
 
 // One NTT of 2^log_n points block-distributed over the communicator's ranks
 // (this rank holds points [rank*m, (rank+1)*m), m = 2^log_n / size); in place.
-int ecg_fft_dist(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omega, uint32_t log_n) {
+int ecg_fft_dist_ex(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omega, uint32_t log_n,
+                    ecg_abort_cb abort_cb, void* user) {
   ECG_ENTER(ctx);
-  if (!d_local || !omega) {
-    set_error("ecg_fft_dist: null pointer");
-    return ECG_ERR_INVALID;
-  }
-  ECG_TRY(dfft_run(ctx, field_id, d_local, omega, log_n, ctx->stream));
-  ECG_HIP(hipStreamSynchronize(ctx->stream));
+  ECG_TRY(dfft_run(ctx, field_id, d_local, omega, log_n, ctx->stream, abort_cb, user));
+  ECG_TRY(comm_wait(ctx, ctx->stream, "ecg_fft_dist"));
   return kt_collect(ctx);
+}
+
+int ecg_fft_dist(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omega, uint32_t log_n) {
+  return ecg_fft_dist_ex(ctx, field_id, d_local, omega, log_n, nullptr, nullptr);
 }
 
 // The two local steps of ecg_fft_dist, exposed so a caller (or a test with

@@ -89,10 +89,15 @@ struct ecg_ctx {
   // MSM terms per device pass (SingleMultiexpKernel::n, multiexp.rs:71-93);
   // 0 = derived from device memory (msm_chunk_terms)
   size_t msm_chunk = 0;
-  // RCCL communicator of this rank (comm.cpp); size 1 / null = single GPU
+  // RCCL communicator of this rank (comm.cpp); size 1 / null = single GPU.
+  // A host transport (ecg_comm_init_host) replaces it when xchg is set.
+  // comm_size > 1 with neither = a communicator aborted after a failure.
   void* comm = nullptr;
   int comm_size = 1;
   int comm_rank = 0;
+  ecg_xchg_cb xchg = nullptr;
+  void* xchg_user = nullptr;
+  uint32_t comm_timeout_ms = 0;  // 0 = ECG_COMM_TIMEOUT_S or the default
   // kernel timing (HIP events on the launch stream)
   std::map<std::string, ecg::KernelTimes> ktimes;
   std::vector<hipEvent_t> event_pool;
@@ -141,10 +146,20 @@ int ecfft_run(ecg_ctx* ctx, int curve_id, void* d_jac, const uint64_t* omega, ui
 int dfft_stage1(int field_id, const void* d_in, void* d_out, const uint64_t* omega, uint32_t T, uint32_t rank,
                 uint32_t log_n, hipStream_t s);
 int dfft_stage3(const void* d_in, void* d_out, uint32_t T, uint32_t log_n, hipStream_t s);
-int dfft_run(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omega, uint32_t log_n, hipStream_t s);
+int dfft_run(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omega, uint32_t log_n, hipStream_t s,
+             ecg_abort_cb abort_cb, void* user);
+const char* last_error_text();  // this thread's last error message
 int comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes_per_peer, hipStream_t s);
 void comm_free(ecg_ctx* ctx);
 int comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes, hipStream_t s);
+// Wait for s (collectives included) under the communicator's deadline; on a
+// timeout or a collective error the communicator is aborted.
+int comm_wait(ecg_ctx* ctx, hipStream_t s, const char* what);
+// Every rank's local return code -> the same code on every rank: ECG_OK if
+// all ranks are ok, else the code of the lowest failing rank (the local
+// message is kept on that rank, the others name it).  `agree` words (e.g.
+// field, size) must match across ranks, else ECG_ERR_INVALID everywhere.
+int comm_agree(ecg_ctx* ctx, int local_rc, const uint64_t* agree, int n_agree, const char* what, hipStream_t s);
 // Bases [x, y] -> a new device buffer in the bucket kernels' layout,
 // registered in the process-wide prepared-bases registry (msm.hip).
 // How the bucket kernels read d_bases: the boundary [x, y] layout, prepared
@@ -175,8 +190,9 @@ int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_base
 int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac);
 int msm_pass_terms_run(const ecg_ctx* ctx, int curve_id, size_t* out);
 // MSM over host slices, uploads pipelined with compute (msm_host_t)
-int msm_host_run(ecg_ctx* ctx, int curve_id, const void* h_bases, const void* h_scalars, size_t n, uint64_t* out_jac,
-                 ecg_abort_cb abort_cb, void* user);
+// bases_resident: `bases` is a device prepared buffer (only the scalars travel)
+int msm_host_run(ecg_ctx* ctx, int curve_id, const void* bases, int bases_resident, const void* h_scalars, size_t n,
+                 int scalar_mont, uint64_t* out_jac, ecg_abort_cb abort_cb, void* user);
 int gen_bases_run(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n,
                   void* d_out, hipStream_t s);
 

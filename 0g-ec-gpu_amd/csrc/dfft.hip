@@ -132,20 +132,35 @@ int dfft_stage3(const void* d_in, void* d_out, uint32_t T, uint32_t log_n, hipSt
 // w^T in Montgomery form (host): omega of the local m-point NTT.
 static void pow2k_host(int field_id, const uint64_t* omega, uint32_t k, uint64_t* out);
 
-int dfft_run(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omega, uint32_t log_n, hipStream_t s) {
+// Every local failure (arguments, workspace, the local NTT, abort_cb) is
+// exchanged (comm_agree) before the all-to-all that would otherwise leave the
+// peers waiting for this rank: once before the first, once before the last.
+int dfft_run(ecg_ctx* ctx, int field_id, void* d_local, const uint64_t* omega, uint32_t log_n, hipStream_t s,
+             ecg_abort_cb abort_cb, void* user) {
   const uint32_t T = (uint32_t)ctx->comm_size, rank = (uint32_t)ctx->comm_rank;
-  uint32_t lt;
-  ECG_TRY(dfft_check(field_id, T, log_n, &lt));
-  const size_t m = (size_t)1 << (log_n - lt);
+  uint32_t lt = 0;
+  void* b = nullptr;
+  int rc = ECG_OK;
+  if (!d_local || !omega) {
+    set_error("ecg_fft_dist: null pointer");
+    rc = ECG_ERR_INVALID;
+  } else {
+    rc = dfft_check(field_id, T, log_n, &lt);
+  }
+  const size_t m = rc == ECG_OK ? (size_t)1 << (log_n - lt) : 0;
+  if (rc == ECG_OK) rc = ws_get(ctx, "dfft_b", m * 32, &b);
+  if (rc == ECG_OK && abort_cb && abort_cb(user)) rc = ECG_ABORTED;  // fft.rs:94-98
+  const uint64_t agree[2] = {(uint64_t)(uint32_t)field_id, log_n};
+  ECG_TRY(comm_agree(ctx, rc, agree, 2, "ecg_fft_dist", s));
   const size_t seg_bytes = (m / T) * 32;
-  void* b;
-  ECG_TRY(ws_get(ctx, "dfft_b", m * 32, &b));
   ECG_TRY(comm_alltoall(ctx, d_local, b, seg_bytes, s));
   ECG_TRY(dfft_stage1(field_id, b, d_local, omega, T, rank, log_n, s));
   ECG_TRY(comm_alltoall(ctx, d_local, b, seg_bytes, s));
   uint64_t om_t[4];
   pow2k_host(field_id, omega, lt, om_t);
-  ECG_TRY(ntt_run(ctx, field_id, b, om_t, log_n - lt, s, nullptr, nullptr));
+  rc = ntt_run(ctx, field_id, b, om_t, log_n - lt, s, nullptr, nullptr);
+  if (rc == ECG_OK && abort_cb && abort_cb(user)) rc = ECG_ABORTED;
+  ECG_TRY(comm_agree(ctx, rc, agree, 2, "ecg_fft_dist", s));
   ECG_TRY(comm_alltoall(ctx, b, d_local, seg_bytes, s));
   ECG_TRY(dfft_stage3(d_local, b, T, log_n, s));
   ECG_HIP(hipMemcpyAsync(d_local, b, m * 32, hipMemcpyDeviceToDevice, s));

@@ -34,6 +34,8 @@ void set_error(const char* fmt, ...) {
   g_err = buf;
 }
 
+const char* last_error_text() { return g_err.c_str(); }
+
 int ctx_enter(ecg_ctx* ctx) {
   if (!ctx) {
     set_error("null context");
@@ -281,10 +283,6 @@ static int fft_batch(ecg_ctx* ctx, int field_id, uint64_t** inouts, const uint64
   ECG_TRY(ws_get(ctx, "fft_io", cnt * bytes, &d));
   hipStream_t s = ctx->stream;
   for (size_t b = 0; b < cnt; b++) {
-    if (!inouts[b]) {
-      set_error("ecg_fft_many: null pointer");
-      return ECG_ERR_INVALID;
-    }
     ECG_HIP(hipMemcpyAsync((uint8_t*)d + b * bytes, inouts[b], bytes, hipMemcpyHostToDevice, s));  // fft.rs:89
   }
   int rc = ntt_run(ctx, field_id, d, omega, log_n, s, abort_cb, user, (uint32_t)cnt);
@@ -298,6 +296,22 @@ static int fft_batch(ecg_ctx* ctx, int field_id, uint64_t** inouts, const uint64
   return kt_collect(ctx);
 }
 
+// Every pointer a *_many call dereferences, checked before any worker starts
+// (the batch helpers then only see valid inputs).
+static int many_args_ok(const char* what, uint64_t** inouts, const uint64_t* omegas, const uint32_t* log_ns,
+                        size_t count) {
+  if (!inouts || !omegas || !log_ns) {
+    set_error("%s: null pointer", what);
+    return ECG_ERR_INVALID;
+  }
+  for (size_t i = 0; i < count; i++)
+    if (!inouts[i]) {
+      set_error("%s: null pointer (input %zu)", what, i);
+      return ECG_ERR_INVALID;
+    }
+  return ECG_OK;
+}
+
 int ecg_fft_many(ecg_ctx** ctxs, int nctx, int field_id, uint64_t** inouts, const uint64_t* omegas,
                  const uint32_t* log_ns, size_t count, ecg_abort_cb abort_cb, void* user) {
   if (!ctxs || nctx <= 0) {
@@ -305,6 +319,7 @@ int ecg_fft_many(ecg_ctx** ctxs, int nctx, int field_id, uint64_t** inouts, cons
     return ECG_ERR_NODEV;
   }
   if (count == 0) return ECG_OK;
+  ECG_TRY(many_args_ok("ecg_fft_many", inouts, omegas, log_ns, count));
   const size_t chunk = (count + nctx - 1) / nctx;  // fft.rs:216
   std::atomic<int> first_err{ECG_OK};
   std::mutex mu;
@@ -381,8 +396,10 @@ int ecg_ec_fft_dev(ecg_ctx* ctx, int curve_id, void* d_inout_jac, const uint64_t
 // transforms 0g runs are latency-bound at under one wave per SIMD each.
 static size_t ecfft_batch_points() {  // points per batched run (A/B: ECG_ECFFT_BATCH_LOG)
   static const size_t v = [] {
+    // clamped to [1, 24]: batch << log_n and the stores' counts stay below 2^32 points
     const char* e = getenv("ECG_ECFFT_BATCH_LOG");
-    return (size_t)1 << (e ? atoi(e) : 20);
+    const int v = e ? atoi(e) : 20;
+    return (size_t)1 << (v >= 1 && v <= 24 ? v : 20);
   }();
   return v;
 }
@@ -395,10 +412,6 @@ static int ec_fft_batch(ecg_ctx* ctx, int curve_id, uint64_t** inouts, const uin
   ECG_TRY(ws_get(ctx, "ecfft_io", cnt * bytes, &d));
   hipStream_t s = ctx->stream;
   for (size_t b = 0; b < cnt; b++) {
-    if (!inouts[b]) {
-      set_error("ecg_ec_fft_many: null pointer");
-      return ECG_ERR_INVALID;
-    }
     ECG_HIP(hipMemcpyAsync((uint8_t*)d + b * bytes, inouts[b], bytes, hipMemcpyHostToDevice, s));  // ec_fft.rs:103
   }
   int rc = ecfft_run(ctx, curve_id, d, omega, log_n, s, abort_cb, user, (uint32_t)cnt);
@@ -419,6 +432,7 @@ int ecg_ec_fft_many(ecg_ctx** ctxs, int nctx, int curve_id, uint64_t** inouts, c
     return ECG_ERR_NODEV;
   }
   if (count == 0) return ECG_OK;
+  ECG_TRY(many_args_ok("ecg_ec_fft_many", inouts, omegas, log_ns, count));
   const size_t chunk = (count + nctx - 1) / nctx;  // ec_fft.rs:231
   std::atomic<int> first_err{ECG_OK};
   std::mutex mu;
@@ -468,7 +482,7 @@ static int msm_host(ecg_ctx* ctx, int curve_id, const uint64_t* bases_xy, const 
   }
   // multiexp.rs:163-164 copies the slices in; here the copies are pipelined
   // with the compute pass by pass (msm_host_t)
-  ECG_TRY(msm_host_run(ctx, curve_id, bases_xy, scalars, n, out_jac, abort_cb, user));
+  ECG_TRY(msm_host_run(ctx, curve_id, bases_xy, 0, scalars, n, 0, out_jac, abort_cb, user));
   return kt_collect(ctx);
 }
 
@@ -575,9 +589,13 @@ int ecg_multiple_multiexp(ecg_ctx* ctx, int curve_id, const void* d_bases, size_
   return kt_collect(ctx);
 }
 
+// Cached bases are prepared buffers (registry-owned); release accordingly.
+static void base_cache_release(void* dev) {
+  if (dev && !msm_prepared_free(dev)) (void)hipFree(dev);
+}
+
 static void base_cache_free(ecg_ctx* ctx) {
-  for (auto& e : ctx->base_cache)
-    if (e.dev) (void)hipFree(e.dev);
+  for (auto& e : ctx->base_cache) base_cache_release(e.dev);
   ctx->base_cache.clear();
 }
 
@@ -622,10 +640,13 @@ static uint64_t bases_fingerprint(const void* host, size_t n, size_t rec_bytes) 
   return h;
 }
 
-// Bases [x, y] on the device for (bases, layout, n): from the cache, or
-// uploaded (and converted from the ark layout) into `slot`.
+// Bases on the device for (bases, layout, n).  Uncached: uploaded (and
+// converted from the ark layout) into the workspace slot `slot` as [x, y].
+// Cached: kept as a prepared buffer (msm_prepare_run: the records the bucket
+// kernels gather), so a cache hit runs as a prepared MSM; the [x, y] staging
+// copy is released after the conversion.
 static int stage_bases(ecg_ctx* ctx, int curve_id, const void* bases, int layout, size_t n, int cache,
-                       const char* slot, void** d_xy) {
+                       const char* slot, void** d_out) {
   const size_t lq = fq_limbs64(curve_id);
   const size_t xy_bytes = n * 2 * lq * 8;
   const size_t raw_bytes = layout == ECG_BASES_ARK_AFFINE ? n * (2 * lq + 1) * 8 : xy_bytes;
@@ -638,48 +659,49 @@ static int stage_bases(ecg_ctx* ctx, int curve_id, const void* bases, int layout
       auto& e = ctx->base_cache[k];
       if (e.host == bases && e.n == n && e.curve == curve_id && e.layout == layout) {
         if (e.fingerprint == fp) {
-          *d_xy = e.dev;
+          *d_out = e.dev;
           return ECG_OK;
         }
         ECG_HIP(hipStreamSynchronize(s));  // same address, other content: drop the stale entry
-        (void)hipFree(e.dev);
+        base_cache_release(e.dev);
         ctx->base_cache.erase(ctx->base_cache.begin() + k);
         break;
       }
     }
   }
-  void* dst;
-  if (cache) {
-    hipError_t e = hipMalloc(&dst, xy_bytes ? xy_bytes : 16);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      set_error("base cache: device allocation of %zu bytes failed: %s", xy_bytes, hipGetErrorString(e));
-      return ECG_ERR_NOMEM;
-    }
-  } else {
-    ECG_TRY(ws_get(ctx, slot, xy_bytes, &dst));
-  }
+  const char* xy_slot = cache ? "cache_stage_xy" : slot;
+  void* xy;
+  ECG_TRY(ws_get(ctx, xy_slot, xy_bytes, &xy));
   if (n) {
     if (layout == ECG_BASES_ARK_AFFINE) {
       void* raw;
       ECG_TRY(ws_get(ctx, "prep_ark_raw", raw_bytes, &raw));
       ECG_HIP(hipMemcpyAsync(raw, bases, raw_bytes, hipMemcpyHostToDevice, s));
-      ECG_TRY(bases_from_ark(ctx, curve_id, raw, n, dst, s));
+      ECG_TRY(bases_from_ark(ctx, curve_id, raw, n, xy, s));
     } else {
-      ECG_HIP(hipMemcpyAsync(dst, bases, xy_bytes, hipMemcpyHostToDevice, s));
+      ECG_HIP(hipMemcpyAsync(xy, bases, xy_bytes, hipMemcpyHostToDevice, s));
     }
   }
-  if (cache) {
-    if (ctx->base_cache.size() >= 8) {  // bounded: drop the oldest entry
-      ECG_HIP(hipStreamSynchronize(s));
-      (void)hipFree(ctx->base_cache.front().dev);
-      ctx->base_cache.erase(ctx->base_cache.begin());
-    }
-    ctx->base_cache.push_back({bases, n, curve_id, layout, dst, fp});
+  if (!cache) {
+    *d_out = xy;
+    return ECG_OK;
   }
-  *d_xy = dst;
+  void* prep = nullptr;
+  ECG_TRY(msm_prepare_run(ctx, curve_id, xy, n, 0, &prep, s));  // synchronises s
+  ws_release(ctx, "cache_stage_xy");
+  ws_release(ctx, "prep_ark_raw");
+  if (ctx->base_cache.size() >= 8) {  // bounded: drop the oldest entry
+    base_cache_release(ctx->base_cache.front().dev);
+    ctx->base_cache.erase(ctx->base_cache.begin());
+  }
+  ctx->base_cache.push_back({bases, n, curve_id, layout, prep, fp});
+  *d_out = prep;
   return ECG_OK;
 }
+
+// Cached bases and host exponents of at least this many terms: the exponents
+// go up in passes overlapped with the previous pass's compute (msm_host_run).
+constexpr size_t MSMX_PIPE_MIN = (size_t)1 << 22;
 
 int ecg_msm_ex(ecg_ctx* ctx, int curve_id, const void* bases, int bases_layout, size_t n_bases, size_t skip,
                const uint64_t* exps, int exps_montgomery, size_t n_exps, const uint64_t* density, int cache_bases,
@@ -698,6 +720,20 @@ int ecg_msm_ex(ecg_ctx* ctx, int curve_id, const void* bases, int bases_layout, 
     return ECG_ERR_INVALID;
   }
   hipStream_t s = ctx->stream;
+  if (cache_bases && !density && n_exps >= MSMX_PIPE_MIN) {
+    // resident bases: only the exponents travel, pass by pass behind the compute
+    if (skip > n_bases || n_exps > n_bases - skip) {
+      set_error("Expected more bases from source.");  // multiexp_cpu.rs:55-61
+      return ECG_ERR_INVALID;
+    }
+    void* d_prep;
+    ECG_TRY(stage_bases(ctx, curve_id, bases, bases_layout, n_bases, 1, nullptr, &d_prep));
+    const uint8_t* b0 = (const uint8_t*)d_prep + skip * msm_prepared_stride(curve_id, 0);
+    int rc = msm_host_run(ctx, curve_id, b0, 1, exps, n_exps, exps_montgomery, out_jac, abort_cb, user);
+    (void)hipStreamSynchronize(s);
+    if (rc != ECG_OK) return rc;
+    return kt_collect(ctx);
+  }
   // exps -> device, density-compacted on device (generate_exps)
   void *d_e, *d_ec;
   ECG_TRY(ws_get(ctx, "msmx_exps", n_exps * 32, &d_e));
@@ -720,9 +756,9 @@ int ecg_msm_ex(ecg_ctx* ctx, int curve_id, const void* bases, int bases_layout, 
   const size_t lq = fq_limbs64(curve_id);
   void* d_xy;
   const uint8_t* d_base0;
-  if (cache_bases) {
+  if (cache_bases) {  // a prepared buffer: base-aligned offset in its record stride
     ECG_TRY(stage_bases(ctx, curve_id, bases, bases_layout, n_bases, 1, nullptr, &d_xy));
-    d_base0 = (const uint8_t*)d_xy + skip * 2 * lq * 8;
+    d_base0 = (const uint8_t*)d_xy + skip * msm_prepared_stride(curve_id, 0);
   } else {
     const size_t rec = bases_layout == ECG_BASES_ARK_AFFINE ? (2 * lq + 1) * 8 : 2 * lq * 8;
     ECG_TRY(stage_bases(ctx, curve_id, (const uint8_t*)bases + skip * rec, bases_layout, dense, 0, "msmx_bases",

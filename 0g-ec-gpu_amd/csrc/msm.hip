@@ -69,9 +69,17 @@ static int prepared_lookup(ecg_ctx* ctx, int curve_id, const void* d_bases, size
     start = it->first;
     e = it->second;
   }
-  // still our allocation?  (header written at prepare time)
+  // still our allocation?  The header is read only while header and records
+  // still lie inside one live device allocation (a released range may be
+  // unmapped, or reused by an allocation that starts elsewhere); then it must
+  // carry this buffer's magic and nonce.
   uint64_t hdr[2] = {0, 0};
-  if (hipMemcpy(hdr, (const void*)(start - PREP_HEADER), sizeof hdr, hipMemcpyDeviceToHost) != hipSuccess ||
+  hipDeviceptr_t alloc_base = nullptr;
+  size_t alloc_size = 0;
+  const uintptr_t h0 = start - PREP_HEADER, h1 = start + e.n * e.stride;
+  const bool live = hipMemGetAddressRange(&alloc_base, &alloc_size, (hipDeviceptr_t)h0) == hipSuccess &&
+                    (uintptr_t)alloc_base <= h0 && h1 <= (uintptr_t)alloc_base + alloc_size;
+  if (!live || hipMemcpy(hdr, (const void*)(start - PREP_HEADER), sizeof hdr, hipMemcpyDeviceToHost) != hipSuccess ||
       hdr[0] != PREP_MAGIC || hdr[1] != e.nonce) {
     (void)hipGetLastError();
     std::lock_guard<std::mutex> g(g_prep_mu);
@@ -249,15 +257,23 @@ int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count
   return point_sum_host(curve_id, pts.data(), count, out_jac);
 }
 
-int msm_host_run(ecg_ctx* ctx, int curve_id, const void* h_bases, const void* h_scalars, size_t n, uint64_t* out_jac,
-                 ecg_abort_cb abort_cb, void* user) {
+int msm_host_run(ecg_ctx* ctx, int curve_id, const void* bases, int bases_resident, const void* h_scalars, size_t n,
+                 int scalar_mont, uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
   if (n > 0x7fffffffull) {
     set_error("multiexp: at most 2^31-1 terms per call");
     return ECG_ERR_INVALID;
   }
   const MsmOps* o = msm_ops(curve_id, "multiexp");
   if (!o) return ECG_ERR_INVALID;
-  return o->host(ctx, h_bases, h_scalars, n, out_jac, abort_cb, user);
+  BaseForm bf;
+  if (bases_resident) {  // must be (a base-aligned view into) a prepared buffer
+    ECG_TRY(prepared_lookup(ctx, curve_id, bases, n, "multiexp", &bf));
+    if (!bf.prepared) {
+      set_error("multiexp: resident bases must be a prepared buffer");
+      return ECG_ERR_INVALID;
+    }
+  }
+  return o->host(ctx, bases, bf, h_scalars, n, scalar_mont ? 1u : 0u, out_jac, abort_cb, user);
 }
 
 int msm_pass_terms_run(const ecg_ctx* ctx, int curve_id, size_t* out) {

@@ -1442,7 +1442,7 @@ size_t msm_pass_terms(const ecg_ctx* ctx) {
                           2.0 * pl.W / pl.seg * (sizeof(XYZZ<AF>) + 4) * (1.0 + 1.0 / 16);
   const double fixed = (double)pl.W * pl.B * sizeof(XYZZ<AF>) + 256.0 * (1 << 20);
   double cached = 0;
-  for (const auto& e : ctx->base_cache) cached += (double)e.n * 2 * sizeof(F);
+  for (const auto& e : ctx->base_cache) cached += (double)e.n * msm_base_record_bytes<C>();  // prepared entries
   const double budget = (double)ctx->mem_bytes * (1.0 - MSM_MEMORY_PADDING) - cached - fixed;
   double t = budget / per_term;
   if (!(t >= (double)(1u << 16))) t = (double)(1u << 16);  // tiny / unknown memory: still make progress
@@ -1501,9 +1501,12 @@ static uint32_t msm_h2d_passes() {  // host-slice pipeline depth (A/B: ECG_MSM_H
 // accumulation is VALU-bound, the copy is PCIe-bound).  Each pass leaves its
 // W window sums in a device array; one D2H and the host Horner folds follow
 // the last pass.  Same group element as the single-pass MSM.
+// bf.prepared: `bases` is a device-resident prepared buffer (the base cache of
+// ecg_msm_ex, an Arc<Vec<G>> seen again): only the 32-B scalars travel, and
+// they still overlap the previous pass's compute.
 template <class C>
-int msm_host_t(ecg_ctx* ctx, const void* h_bases, const void* h_scalars, size_t n, uint64_t* out_jac,
-               ecg_abort_cb abort_cb, void* user) {
+int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scalars, size_t n, uint32_t scalar_mont,
+               uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
   using F = typename C::Fq;
   using X = XYZZ<F>;
   using HX = host::HPoint<HostF<C>>;
@@ -1512,6 +1515,7 @@ int msm_host_t(ecg_ctx* ctx, const void* h_bases, const void* h_scalars, size_t 
     host::hto_jac_norm(HX::zero(), out_jac);
     return ECG_OK;
   }
+  const bool resident = bf.prepared;
   const size_t bb = 2 * sizeof(F), sb = 32;
   size_t pass = msm_pass_terms<C>(ctx);
   if (n >= ((size_t)1 << 22)) {
@@ -1523,14 +1527,17 @@ int msm_host_t(ecg_ctx* ctx, const void* h_bases, const void* h_scalars, size_t 
   std::vector<size_t> woff(np + 1, 0);
   for (size_t k = 0; k < np; k++) {
     const size_t m = std::min(pass, n - k * pass);
-    plans[k] = make_plan(m, (uint32_t)C::FrParams::BITS);
-    woff[k + 1] = woff[k] + plans[k].W;
+    plans[k] = bf.tab_c ? make_tab_plan(1, (uint32_t)C::FrParams::BITS, bf.tab_c, bf.tab_n)
+                        : make_plan(m, (uint32_t)C::FrParams::BITS);
+    woff[k + 1] = woff[k] + plans[k].fold_windows();
   }
+  // bytes per base of the resident buffer (all of its table rows)
+  const size_t rstride = msm_base_record_bytes<C>() * (bf.tab_c ? msm_table_windows<C>(bf.tab_c) : 1u);
   void *ib[2] = {nullptr, nullptr}, *is[2] = {nullptr, nullptr}, *sums;
-  ECG_TRY(ws_get(ctx, "msm_in_bases", pass * bb, &ib[0]));
+  if (!resident) ECG_TRY(ws_get(ctx, "msm_in_bases", pass * bb, &ib[0]));
   ECG_TRY(ws_get(ctx, "msm_in_scalars", pass * sb, &is[0]));
   if (np > 1) {
-    ECG_TRY(ws_get(ctx, "msm_in_bases_b", pass * bb, &ib[1]));
+    if (!resident) ECG_TRY(ws_get(ctx, "msm_in_bases_b", pass * bb, &ib[1]));
     ECG_TRY(ws_get(ctx, "msm_in_scalars_b", pass * sb, &is[1]));
   }
   ECG_TRY(ws_get(ctx, "msm_pass_sums", woff[np] * sizeof(X), &sums));
@@ -1544,7 +1551,8 @@ int msm_host_t(ecg_ctx* ctx, const void* h_bases, const void* h_scalars, size_t 
   auto upload = [&](size_t k) -> int {
     const size_t off = k * pass, m = std::min(pass, n - off);
     const int b = (int)(k & 1);
-    ECG_HIP(hipMemcpyAsync(ib[b], (const uint8_t*)h_bases + off * bb, m * bb, hipMemcpyHostToDevice, us));
+    if (!resident)
+      ECG_HIP(hipMemcpyAsync(ib[b], (const uint8_t*)bases + off * bb, m * bb, hipMemcpyHostToDevice, us));
     ECG_HIP(hipMemcpyAsync(is[b], (const uint8_t*)h_scalars + off * sb, m * sb, hipMemcpyHostToDevice, us));
     ECG_HIP(hipEventRecord(up[b], us));
     return ECG_OK;
@@ -1557,12 +1565,14 @@ int msm_host_t(ecg_ctx* ctx, const void* h_bases, const void* h_scalars, size_t 
     }
     const int b = (int)(k & 1);
     const size_t m = std::min(pass, n - k * pass);
-    const MsmGeom g{1, 1, m, m, 0};
+    const MsmGeom g{1, 1, m, m, scalar_mont};
     void* d_sums = nullptr;
+    const void* bp = resident ? (const void*)((const uint8_t*)bases + k * pass * rstride) : ib[b];
     rc = [&]() -> int {
       ECG_HIP(hipStreamWaitEvent(cs, up[b], 0));
-      ECG_TRY(msm_core_t<C>(ctx, ib[b], is[b], g, plans[k], cs, &d_sums));
-      ECG_HIP(hipMemcpyAsync((X*)sums + woff[k], d_sums, plans[k].W * sizeof(X), hipMemcpyDeviceToDevice, cs));
+      ECG_TRY(msm_core_t<C>(ctx, bp, is[b], g, plans[k], cs, &d_sums, resident));
+      ECG_HIP(hipMemcpyAsync((X*)sums + woff[k], d_sums, plans[k].fold_windows() * sizeof(X),
+                             hipMemcpyDeviceToDevice, cs));
       ECG_HIP(hipEventRecord(done[b], cs));
       if (k + 1 < np) {
         if (k >= 1) ECG_HIP(hipStreamWaitEvent(us, done[b ^ 1], 0));  // pass k-1 has released its staging half

@@ -19,8 +19,10 @@ struct MsmOps {
   int (*point_sum)(const uint64_t* points, size_t count, uint64_t* out_jac);
   int (*gen_bases)(ecg_ctx*, const uint64_t* a, const uint64_t* b, size_t n, void* d_out, hipStream_t);
   size_t (*pass_terms)(const ecg_ctx*);
-  int (*host)(ecg_ctx*, const void* h_bases, const void* h_scalars, size_t n, uint64_t* out_jac, ecg_abort_cb,
-              void* user);
+  // host scalars, pipelined with compute; bases on the host ([x, y]), or with
+  // bf.prepared a device-resident prepared buffer
+  int (*host)(ecg_ctx*, const void* bases, BaseForm bf, const void* h_scalars, size_t n, uint32_t scalar_mont,
+              uint64_t* out_jac, ecg_abort_cb, void* user);
   size_t (*record_bytes)();  // bytes per prepared base record (one table row)
   int (*plan_info)(size_t n, uint32_t window_bits, uint32_t* c, uint32_t* windows, int* sort_mode);
 };

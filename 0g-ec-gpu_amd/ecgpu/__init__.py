@@ -48,6 +48,10 @@ ECG_ERR_INVALID, ECG_ERR_HIP, ECG_ERR_NOMEM, ECG_ERR_NODEV, ECG_ERR_RCCL = -1, -
 
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 ABORT_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+# ecg_xchg_cb(op, send, recv, bytes, user): the host transport of ecg_comm_init_host
+XCHG_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                           ctypes.c_void_p)
+XCHG_ALLGATHER, XCHG_ALLTOALL = 0, 1
 
 # ---------------------------------------------------------------------------
 # errors (ec-gpu-program/src/lib.rs:10-32)
@@ -124,7 +128,13 @@ _SIGS = {
     "ecg_comm_alltoall": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]),
     "ecg_msm_dist": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                     _u64p]),
+    "ecg_msm_dist_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_size_t, _u64p, ABORT_CB, ctypes.c_void_p]),
     "ecg_fft_dist": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, _u64p, ctypes.c_uint32]),
+    "ecg_fft_dist_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, _u64p, ctypes.c_uint32,
+                                       ABORT_CB, ctypes.c_void_p]),
+    "ecg_comm_set_timeout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    "ecg_comm_init_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, XCHG_CB, ctypes.c_void_p]),
     "ecg_fft_dist_stage1": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, _u64p,
                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     "ecg_fft_dist_stage3": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,

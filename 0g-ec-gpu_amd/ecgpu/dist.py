@@ -294,12 +294,16 @@ def msm_sharded(n: int, partial_fn: Callable[[int, int], "object"], fold_fn: Cal
 
 
 def comm_init(prog, rank: int, world: int, broadcast: Callable[[Any], Any] | None = None,
-              make_id: Callable[[], bytes] | None = None) -> bytes:
+              make_id: Callable[[], bytes] | None = None, rccl_at_world1: bool = False,
+              timeout_s: float | None = None) -> bytes:
     """Rank 0 makes the RCCL id (make_id, default ecg_comm_unique_id), the
     launcher's group broadcasts it (broadcast(obj) -> rank 0's obj, e.g.
     HostGroup.broadcast), every rank binds its Program's context
     (ecg_comm_init).  make_id is injectable so the CPU tests run the same
-    exchange without RCCL.  Returns the 128-byte id every rank used."""
+    exchange without RCCL.  At world 1 no communicator is made unless
+    rccl_at_world1 (a real one-rank RCCL communicator: the RCCL code path on a
+    one-GPU box).  timeout_s bounds initialisation and every exchange
+    (ecg_comm_set_timeout).  Returns the 128-byte id every rank used."""
     import ctypes
 
     import ecgpu
@@ -316,10 +320,91 @@ def comm_init(prog, rank: int, world: int, broadcast: Callable[[Any], Any] | Non
         if not isinstance(ident, (bytes, bytearray)) or len(ident) != 128:
             raise ValueError("comm_init: the broadcast RCCL id must be 128 bytes")
         ctypes.memmove(buf, bytes(ident), 128)
+    elif rccl_at_world1:
+        ctypes.memmove(buf, make_id() if make_id is not None else unique_id(), 128)
     if prog is None:  # exchange only (CPU tests)
         return bytes(buf)
-    ecgpu._check(ecgpu.lib().ecg_comm_init(prog.handle, world, rank, buf), "comm_init")
+    L = ecgpu.lib()
+    if timeout_s is not None:
+        ecgpu._check(L.ecg_comm_set_timeout(prog.handle, int(timeout_s * 1000)), "comm_set_timeout")
+    ecgpu._check(L.ecg_comm_init(prog.handle, world, rank, buf if world > 1 or rccl_at_world1 else None),
+                 "comm_init")
     return bytes(buf)
+
+
+def comm_init_host(prog, rank: int, world: int, exchange: Callable[[int, bytes, int], bytes],
+                   timeout_s: float | None = None) -> None:
+    """Bind prog's context to a host transport (ecg_comm_init_host) instead of
+    RCCL: exchange(op, send, nbytes) -> recv bytes, with op XCHG_ALLGATHER
+    (send = nbytes, recv = world x nbytes in rank order) or XCHG_ALLTOALL
+    (send = world x nbytes, block q to rank q; recv block q from rank q).
+    For ranks that share a GPU (RCCL refuses them) and for launchers that
+    already hold a group.  A raising exchange fails the call on this rank."""
+    import ctypes
+
+    import ecgpu
+
+    def cb(op, send, recv, nbytes, _user):
+        try:
+            data = ctypes.string_at(send, nbytes * (world if op == ecgpu.XCHG_ALLTOALL else 1))
+            out = exchange(op, data, nbytes)
+            if len(out) != nbytes * world:
+                return 1
+            ctypes.memmove(recv, out, len(out))
+            return 0
+        except Exception:  # noqa: BLE001 -- any transport failure is a failed exchange
+            return 1
+
+    c_cb = ecgpu.XCHG_CB(cb)
+    prog._xchg_cb = c_cb  # the context keeps calling it: keep it alive with the Program
+    L = ecgpu.lib()
+    if timeout_s is not None:
+        ecgpu._check(L.ecg_comm_set_timeout(prog.handle, int(timeout_s * 1000)), "comm_set_timeout")
+    ecgpu._check(L.ecg_comm_init_host(prog.handle, world, rank, c_cb, None), "comm_init_host")
+
+
+class LocalExchange:
+    """In-process host transport for `world` ranks driven by threads (one
+    context each, e.g. all on one GPU): exchange_for(rank) is the rank's
+    comm_init_host callable.  A rank that does not arrive within timeout_s
+    breaks the barrier and every waiting rank's exchange fails."""
+
+    def __init__(self, world: int, timeout_s: float = 120.0):
+        import threading
+
+        self.world = world
+        self._slots: list = [None] * world
+        self._barrier = threading.Barrier(world, timeout=timeout_s)
+
+    def exchange_for(self, rank: int) -> Callable[[int, bytes, int], bytes]:
+        import ecgpu
+
+        def exchange(op: int, data: bytes, nbytes: int) -> bytes:
+            self._slots[rank] = data
+            self._barrier.wait()
+            if op == ecgpu.XCHG_ALLGATHER:
+                out = b"".join(self._slots)
+            else:
+                out = b"".join(self._slots[q][rank * nbytes:(rank + 1) * nbytes] for q in range(self.world))
+            self._barrier.wait()  # nobody overwrites a slot before every rank has read it
+            return out
+
+        return exchange
+
+
+def hostgroup_exchange(group: "HostGroup") -> Callable[[int, bytes, int], bytes]:
+    """comm_init_host callable over a HostGroup (small exchanges: its frames
+    are capped at 1 MiB)."""
+    import ecgpu
+
+    def exchange(op: int, data: bytes, nbytes: int) -> bytes:
+        blocks = group.allgather(data)
+        if op == ecgpu.XCHG_ALLGATHER:
+            return b"".join(blocks)
+        r = group.rank
+        return b"".join(b[r * nbytes:(r + 1) * nbytes] for b in blocks)
+
+    return exchange
 
 
 def unique_id() -> bytes:
@@ -345,28 +430,37 @@ def torch_broadcast(dist_mod=None, group=None) -> Callable[[Any], Any]:
     return bcast
 
 
-def msm_dist(prog, curve, d_bases, d_scalars, n_local: int):
-    """This rank's shard + RCCL all-gather of partials + fold -> full result."""
+def msm_dist(prog, curve, d_bases, d_scalars, n_local: int, maybe_abort=None):
+    """This rank's shard + all-gather of [status | partial] + fold -> full
+    result on every rank, or the same error on every rank (ecg_msm_dist_ex;
+    maybe_abort polled before each device pass, multiexp.rs:140-144)."""
     import numpy as np
 
     import ecgpu
 
-    cid = ecgpu._curve(curve)
-    out = np.zeros(3 * ecgpu.CURVE_FQ_LIMBS[cid], dtype=np.uint64)
-    ecgpu._check(ecgpu.lib().ecg_msm_dist(prog.handle, cid, d_bases.ptr, d_scalars.ptr, n_local, ecgpu._ptr(out)),
-                 "msm_dist")
+    cid = ecgpu.CURVE_NAMES.get(curve, -1) if isinstance(curve, str) else int(curve)
+    out = np.zeros(3 * ecgpu.CURVE_FQ_LIMBS.get(cid, 12), dtype=np.uint64)
+    cb, keep = ecgpu._abort_cb(maybe_abort)
+    ecgpu._check(ecgpu.lib().ecg_msm_dist_ex(prog.handle, cid, d_bases.ptr if d_bases is not None else None,
+                                             d_scalars.ptr if d_scalars is not None else None, n_local,
+                                             ecgpu._ptr(out), cb, None), "msm_dist")
+    del keep
     return out
 
 
-def fft_dist(prog, field, d_local, omega, log_n: int) -> None:
-    """One 2^log_n NTT, block-distributed over the communicator (in place)."""
+def fft_dist(prog, field, d_local, omega, log_n: int, maybe_abort=None) -> None:
+    """One 2^log_n NTT, block-distributed over the communicator (in place);
+    statuses exchanged before the first and the last all-to-all."""
     import numpy as np
 
     import ecgpu
 
     om = np.ascontiguousarray(omega, dtype=np.uint64).reshape(4)
-    ecgpu._check(ecgpu.lib().ecg_fft_dist(prog.handle, ecgpu._fft_field(field), d_local.ptr, ecgpu._ptr(om), log_n),
-                 "fft_dist")
+    fid = ecgpu.FIELD_NAMES.get(field, -1) if isinstance(field, str) else int(field)
+    cb, keep = ecgpu._abort_cb(maybe_abort)
+    ecgpu._check(ecgpu.lib().ecg_fft_dist_ex(prog.handle, fid, d_local.ptr if d_local is not None else None,
+                                             ecgpu._ptr(om), log_n, cb, None), "fft_dist")
+    del keep
 
 
 def fft_dist_emulated(progs, field, d_blocks, omega, log_n: int) -> None:

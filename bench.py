@@ -405,6 +405,27 @@ def main():
         out_e2e = kern.multiexp(pool, host_bases, scal, 0)
         msm_e2e_s = time.perf_counter() - t_e
         checks["msm_e2e_equals_resident"] = bool((out_e2e == msm_result).all())
+        # as the Rust drop-in calls it (MultiexpKernel::multiexp(pool, Arc<Vec<Affine>>, exps, skip)):
+        # arkworks Affine {x, y, infinity} records straight from the caller, converted on the device and
+        # kept resident in the base cache; the first call uploads and prepares them, the second with the
+        # same array uploads only the exponents (pipelined with the compute)
+        ark = np.zeros((n_loc, 2 * lq + 1), dtype=np.uint64)
+        ark[:, :2 * lq] = host_bases
+        del host_bases
+        kern.clear_base_cache()
+        t_e = time.perf_counter()
+        out_cold = kern.multiexp_ex(ark, scal, 0, ark_affine=True, cache_bases=True)
+        ark_cold_s = time.perf_counter() - t_e
+        ark_cached = []
+        for _ in range(3):
+            t_e = time.perf_counter()
+            out_warm = kern.multiexp_ex(ark, scal, 0, ark_affine=True, cache_bases=True)
+            ark_cached.append(time.perf_counter() - t_e)
+        checks["msm_ark_cached_equals_resident"] = bool((out_cold == msm_result).all()
+                                                        and (out_warm == msm_result).all())
+        kern.clear_base_cache()
+        del ark
+        host_bases = None
         fk = ecgpu.FftKernel.create([prog], args.curve + "_fr")
         host_ntt = ntt_in.copy()
         fk.radix_fft(host_ntt, omega_m, log_n)
@@ -413,9 +434,14 @@ def main():
         fk.radix_fft(host_ntt, omega_m, log_n)
         ntt_e2e_s = time.perf_counter() - t_e
         e2e = {"msm_ms": msm_e2e_s * 1e3, "msm_terms_per_s": n_loc / msm_e2e_s,
+               "msm_ark_cold_ms": ark_cold_s * 1e3, "msm_ark_cached_ms": min(ark_cached) * 1e3,
+               "msm_ark_cached_ms_all": [t * 1e3 for t in ark_cached],
                "ntt_ms": ntt_e2e_s * 1e3, "ntt_elements_per_s": n_ntt / ntt_e2e_s,
-               "note": "host buffers in, host result out (H2D of 128 B/term, NTT H2D+D2H of 32 B/element)"}
-        del host_bases
+               "note": "host buffers in, host result out. msm_ms: GpuRepr [x, y] slices (ecg_msm, H2D of 128 B/term "
+                       "pipelined with compute); msm_ark_*: arkworks Affine records (104 B/base) as the Rust "
+                       "MultiexpKernel::multiexp passes its Arc<Vec<G>> (ecg_msm_ex, ark layout, base cache): "
+                       "cold = upload + device conversion + prepare + MSM, cached = the same Arc again (only the "
+                       "32-B exponents travel, in passes behind the compute); NTT: H2D+D2H of 32 B/element"}
 
     # ------------------------------------------------------------ side lines (N = 1): SURVEY §8f rows
     aux = None
@@ -546,12 +572,12 @@ def main():
     # ------------------------------------------------------------ report
     n_acc = n_loc  # terms per accumulation launch on rank 0 (the largest shard)
     W = -(-(r_int.bit_length() + 1) // 20) if args.msm_log >= 24 else None  # windows at c = 20
-    bytes_per_term = 2 * lq * 8 + 32  # 96 B affine + 32 B scalar (BLS12-381), SURVEY §8(d)
+    bytes_per_term = 2 * lq * 8 + 32  # affine + 32 B scalar: 128 B (BLS12-381), 96 B (BN254), SURVEY §8(d)
     hbm_achieved = bytes_per_term * n_acc / (acc_avg_ms / 1e3) / 1e9
     # the committed PMC passes profile the default (BLS12-381, 2^26 / 2^24) run
     default_run = cid == 0 and args.msm_log == 26 and log_n == 24 and world == 1
-    acc_traffic, acc_src = pmc_traffic("msm_accumulate", streaming_read=False) if default_run else (None, None)
-    ntt_traffic, ntt_src = pmc_traffic("ntt_pass", streaming_read=True) if default_run else (None, None)
+    acc_traffic, acc_src = pmc_traffic("msm_accumulate") if default_run else (None, None)
+    ntt_traffic, ntt_src = pmc_traffic("ntt_pass") if default_run else (None, None)
     ntt_achieved = 64 * n_ntt / (pass_avg_ms / 1e3) / 1e9
     roofline = {"bound": "valu", "kernel": "msm_accumulate", "avg_ms": acc_avg_ms,
                 "traffic": acc_traffic, "traffic_unit": "GB/launch", "traffic_source": acc_src}
@@ -564,7 +590,8 @@ def main():
                                  f"x {W} windows x terms / launch time; peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz"})
     roofline["hbm"] = {"achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": hbm_achieved / HBM_PEAK_GBS,
-                       "note": "algorithmic 128 B/term (96 B base + 32 B scalar) x terms per launch / launch time"}
+                       "note": f"algorithmic {bytes_per_term} B/term ({2 * lq * 8} B base + 32 B scalar) x terms "
+                               "per launch / launch time"}
     line = {
         "metric": "BLS12-381 G1 MSM point-adds/sec @2^26 + Fr NTT elements/sec @2^24"
         if cid == 0 else "BN254 G1 MSM point-adds/sec + Fr NTT elements/sec",
@@ -632,13 +659,14 @@ def _g2_kat(cid: int, scal: np.ndarray, r_int: int, got: np.ndarray) -> bool:
     return po.jac_to_affine((fq2(j[0]), fq2(j[1]), fq2(j[2])), p) == want
 
 
-def pmc_traffic(kernel: str, streaming_read: bool):
+def pmc_traffic(kernel: str):
     """HBM bytes per launch (GB) from the committed rocprofv3 PMC passes
     (tools/gpu.sh prof -> profiles/<round>/pmc_fetch_write.json, copied to
-    profiles/pmc_current.json with its source): FETCH_SIZE + WRITE_SIZE.
-    gfx950 FETCH_SIZE counts half the bytes of wide coalesced streaming reads
-    (MI355X_MICROARCH.md, HBM/rocprofv3 section), so those are doubled;
-    gathers are reported as counted."""
+    profiles/pmc_current.json with its source): 2 x FETCH_SIZE + WRITE_SIZE.
+    gfx950 FETCH_SIZE tallies each 128-B read request at 64 B (TCC_EA0_RDREQ
+    x 64; MI355X_MICROARCH.md, HBM/rocprofv3 section), so it is doubled for
+    both kernels: the NTT's 16-B/lane streaming reads and the accumulation's
+    16-B/lane reads of whole 128-B base records are both 128-B requests."""
     path = os.path.join(ROOT, "profiles", "pmc_current.json")
     if not os.path.exists(path):
         return None, None
@@ -648,7 +676,7 @@ def pmc_traffic(kernel: str, streaming_read: bool):
         if kernel in k:
             fetch = v["FETCH_SIZE"]["mean_kb"] * 1024 / 1e9
             write = v["WRITE_SIZE"]["mean_kb"] * 1024 / 1e9
-            return (2 * fetch if streaming_read else fetch) + write, d["source"]
+            return 2 * fetch + write, d["source"]
     return None, None
 
 

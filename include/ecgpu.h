@@ -310,24 +310,63 @@ int ecg_msm_check_bases(int curve_id, const uint64_t *bases_xy, const uint64_t *
  * Replace the reference's host-thread-per-device dispatch (multiexp.rs:324-367,
  * fft.rs:211-246) for the one-process-per-GPU launch: rank 0 makes a 128-byte
  * id, the launcher broadcasts it, every rank calls ecg_comm_init on its own
- * context.  nranks = 1 needs no id (exchanges become device copies). */
+ * context.  nranks = 1 with a NULL id: no communicator (exchanges become
+ * device copies); with an id: a real one-rank RCCL communicator.
+ *
+ * Failure semantics (the reference stops every device at the first error,
+ * multiexp.rs:345-365, fft.rs:218-245): the distributed calls exchange every
+ * rank's status before their payload collectives, so a rank that fails
+ * locally (bad argument, allocation, abort_cb) makes EVERY rank return an
+ * error instead of leaving its peers blocked in a collective: the lowest
+ * failing rank's code (ECG_ABORTED stays ECG_ABORTED), with the local message
+ * on that rank and "rank k failed" on the others.  The communicator is
+ * non-blocking: initialisation and every collective wait under a deadline
+ * (ecg_comm_set_timeout; default ECG_COMM_TIMEOUT_S or 300 s), after which
+ * the communicator is aborted and the call returns ECG_ERR_RCCL (a peer that
+ * crashed or never arrived).  An aborted communicator refuses later
+ * distributed calls until ecg_comm_init runs again. */
 int ecg_comm_unique_id(uint8_t *out /* 128 bytes */);
 int ecg_comm_init(ecg_ctx *ctx, int nranks, int rank, const uint8_t *unique_id);
 void ecg_comm_destroy(ecg_ctx *ctx);
+/* Deadline of communicator initialisation and of each exchange, in ms
+ * (0 = ECG_COMM_TIMEOUT_S or 300 s).  Applies to the next ecg_comm_init too. */
+int ecg_comm_set_timeout(ecg_ctx *ctx, uint32_t ms);
+/* Host transport instead of RCCL: the caller's launcher group moves the
+ * bytes (e.g. ranks that share a GPU, which RCCL refuses, or a launcher that
+ * already holds an MPI / gloo group).  xchg(op, send, recv, bytes, user)
+ * returns 0 on success:
+ *   ECG_XCHG_ALLGATHER: send = bytes, recv = nranks x bytes in rank order;
+ *   ECG_XCHG_ALLTOALL : send = nranks x bytes (block q goes to rank q),
+ *                       recv = nranks x bytes (block q came from rank q).
+ * Buffers are host memory; the callback runs on the calling thread. */
+#define ECG_XCHG_ALLGATHER 0
+#define ECG_XCHG_ALLTOALL 1
+typedef int (*ecg_xchg_cb)(int op, const void *send, void *recv, size_t bytes, void *user);
+int ecg_comm_init_host(ecg_ctx *ctx, int nranks, int rank, ecg_xchg_cb xchg, void *user);
 /* RCCL all-gather / equal-split all-to-all of device buffers (synchronous). */
 int ecg_comm_allgather(ecg_ctx *ctx, const void *d_send, void *d_recv, size_t bytes);
 int ecg_comm_alltoall(ecg_ctx *ctx, const void *d_send, void *d_recv, size_t bytes_per_peer);
 /* MSM over this rank's contiguous shard (multiexp.rs:332-336 split); the
  * per-rank partial points are all-gathered over RCCL and folded on the host
  * (multiexp.rs:394-397; RCCL has no EC-add reduction), so every rank gets
- * the full result in out_jac (host, 3 x Lq u64). */
+ * the full result in out_jac (host, 3 x Lq u64).  Each rank's status rides
+ * in the same all-gather as its partial (one collective per call). */
 int ecg_msm_dist(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n_local,
                  uint64_t *out_jac);
+/* With the reference's maybe_abort (multiexp.rs:140-144): polled before each
+ * device pass of the local MSM; an abort on any rank returns ECG_ABORTED on
+ * every rank. */
+int ecg_msm_dist_ex(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n_local,
+                    uint64_t *out_jac, ecg_abort_cb abort_cb, void *user);
 /* One NTT of 2^log_n points, block-distributed (rank r holds points
  * [r m, (r+1) m), m = 2^log_n / nranks), in place, natural order: the
  * four-step split of parallel_fft (fft_cpu.rs:59-111) with three RCCL
- * all-to-alls.  nranks a power of two <= 16, 2^log_n >= 2 nranks^2. */
+ * all-to-alls.  nranks a power of two <= 16, 2^log_n >= 2 nranks^2.
+ * Statuses are exchanged before the first all-to-all and after the local
+ * NTT (abort_cb polled at both, as fft.rs:94-98 polls it per pass). */
 int ecg_fft_dist(ecg_ctx *ctx, int field_id, void *d_local, const uint64_t *omega, uint32_t log_n);
+int ecg_fft_dist_ex(ecg_ctx *ctx, int field_id, void *d_local, const uint64_t *omega, uint32_t log_n,
+                    ecg_abort_cb abort_cb, void *user);
 /* Its local steps (for callers that drive the exchanges themselves):
  * stage1: T-point DFT across the received segments + twiddle; stage3: the
  * final [T][m/T] -> [m/T][T] interleave.  See dfft.hip for the layouts. */

@@ -6,7 +6,7 @@ use ark_std::Zero;
 use ecgpu_sys as sys;
 
 use crate::pairing_suite::{Affine, Curve, Scalar};
-use crate::workspace::{check, curve_of, ActiveWorkspace, CudaResult, DeviceData};
+use crate::workspace::{check, curve_of, ActiveWorkspace, CudaError, CudaResult, DeviceData};
 use crate::{GLOBAL, LOCAL};
 
 /// Upload `bases` (their GPU form, [x, y], identity all zero) and convert them
@@ -15,6 +15,30 @@ use crate::{GLOBAL, LOCAL};
 pub fn upload_multiexp_bases(
     workspace: &ActiveWorkspace, bases: &[Affine],
 ) -> CudaResult<DeviceData> {
+    upload_prepared(workspace, bases, None)
+}
+
+/// `upload_multiexp_bases` for bases reused across many batched MSMs (0g's
+/// fixed SRS / AMT bases, benches/amt.rs:18-48): besides the records, the
+/// engine precomputes every base's window multiples 2^(k c) P (ecg_msm_prepare_table),
+/// so each task's windows share one bucket set -- fewer mixed adds per term
+/// and no per-window reduction (AMT shape: 2.65e8 instead of 1.8e8 terms/s).
+/// `chunk_len` is the task length the table is sized for (exponents.len() /
+/// num_chunks of the later `multiple_multiexp` calls); `window_bits = 0` lets
+/// the engine pick the window for it.  Memory: ceil(256 / c) x the records.
+/// Results are identical to the plain upload.
+pub fn upload_multiexp_bases_table(
+    workspace: &ActiveWorkspace, bases: &[Affine], chunk_len: usize, window_bits: u32,
+) -> CudaResult<DeviceData> {
+    let curve = curve_of::<Affine>()?;
+    let c = if window_bits != 0 { window_bits } else { unsafe { sys::ecg_msm_table_window(curve, chunk_len) } };
+    if c == 0 {
+        return Err(CudaError::InvalidValue("no window-table form for this curve".into()));
+    }
+    upload_prepared(workspace, bases, Some(c))
+}
+
+fn upload_prepared(workspace: &ActiveWorkspace, bases: &[Affine], table: Option<u32>) -> CudaResult<DeviceData> {
     let curve = curve_of::<Affine>()?;
     let repr: Vec<_> = bases.iter().map(GpuRepr::to_gpu_repr).collect();
     let bytes = std::mem::size_of_val(&repr[..]);
@@ -24,8 +48,29 @@ pub fn upload_multiexp_bases(
     let staged = DeviceData::from_raw(workspace.program().clone(), staged, bytes, repr.len());
     check(unsafe { sys::ecg_dev_upload(ctx, staged.as_ptr() as *mut _, repr.as_ptr() as *const _, bytes) })?;
     let mut prepared = std::ptr::null_mut();
-    check(unsafe { sys::ecg_msm_prepare_bases(ctx, curve, staged.as_ptr(), repr.len(), &mut prepared) })?;
-    Ok(DeviceData::from_raw(workspace.program().clone(), prepared, bytes, repr.len()))
+    check(unsafe {
+        match table {
+            None => sys::ecg_msm_prepare_bases(ctx, curve, staged.as_ptr(), repr.len(), &mut prepared),
+            Some(c) => sys::ecg_msm_prepare_table(ctx, curve, staged.as_ptr(), repr.len(), c, &mut prepared),
+        }
+    })?;
+    // the device buffer's own size: records (and table rows) per base
+    let stride = unsafe { sys::ecg_msm_prepared_stride(curve, table.unwrap_or(0)) };
+    Ok(DeviceData::from_raw(workspace.program().clone(), prepared, stride * repr.len(), repr.len()))
+}
+
+/// `upload_multiexp_bases_table` on this thread's workspace.
+pub fn upload_multiexp_bases_table_mt(bases: &[Affine], chunk_len: usize, window_bits: u32) -> CudaResult<DeviceData> {
+    LOCAL.with(|w| {
+        let workspace = w.activate()?;
+        upload_multiexp_bases_table(&workspace, bases, chunk_len, window_bits)
+    })
+}
+
+/// `upload_multiexp_bases_table` on the global workspace.
+pub fn upload_multiexp_bases_table_st(bases: &[Affine], chunk_len: usize, window_bits: u32) -> CudaResult<DeviceData> {
+    let workspace = GLOBAL.activate()?;
+    upload_multiexp_bases_table(&workspace, bases, chunk_len, window_bits)
 }
 
 /// `upload_multiexp_bases` on this thread's workspace.

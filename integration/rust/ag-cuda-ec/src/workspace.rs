@@ -98,8 +98,8 @@ impl<'a> ActiveWorkspace<'a> {
 }
 
 /// Bases resident in HBM, owned by the engine.  `size()` is the byte size of
-/// the GPU representation that was uploaded (n x size_of::<Affine::Repr>),
-/// as in the reference, whatever form the engine keeps them in.
+/// the device buffer (prepared records: n x ecg_msm_prepared_stride, which
+/// includes the window-table rows of a table upload); `len()` the bases.
 pub struct DeviceData {
     program: Arc<Program>,
     ptr: *mut c_void,
@@ -119,7 +119,7 @@ impl DeviceData {
         self.ptr
     }
 
-    /// Bytes of the uploaded representation.
+    /// Bytes of the device buffer.
     pub fn size(&self) -> usize {
         self.size
     }

@@ -1,19 +1,80 @@
 //! Multi-scalar multiplication on MI355X (feature `amd`): the public API of
 //! ec-gpu-proxy/src/multiexp.rs (SingleMultiexpKernel 52-252, MultiexpKernel
-//! 256-404) over libecgpu.so's sorted-bucket Pippenger (ecg_msm).
+//! 256-404) over libecgpu.so's sorted-bucket Pippenger.
+//!
+//! The reference converts every base on the host (`to_gpu_repr`, :152-153) and
+//! copies bases and exponents in on every call (:163-164).  Here the caller's
+//! arkworks `Affine { x, y, infinity }` records go to the device as they are
+//! and are converted there (`ecg_msm_ex`, `ECG_BASES_ARK_AFFINE`), and
+//! `MultiexpKernel::multiexp`, which receives the bases as an
+//! `Arc<Vec<G>>` (immutable while shared), asks the engine to keep them
+//! resident in its base cache (`cache_bases`), keyed by address: a second call
+//! with the same `Arc` uploads only the exponents.  The kernel holds a clone
+//! of every `Arc` the engine caches, so no other array can take a cached
+//! address while its entry lives.
 
+use std::os::raw::{c_int, c_void};
 use std::sync::{Arc, RwLock};
 
 use ag_types::{GpuCurveAffine, GpuName, GpuRepr, PrimeFieldRepr as PrimeField};
-use ark_ff::Zero;
+use ark_ec::AffineRepr;
+use ark_ff::{One, Zero};
 use ec_gpu_program::{EcError, EcResult};
 use ecgpu_sys as sys;
-use log::{error, info};
+use log::{error, info, warn};
 use rust_gpu_tools::{Device, Program};
 use yastl::Scope;
 
 use super::{abort_hook, check, curve_id, require, MaybeAbort};
 use crate::threadpool::Worker;
+
+/// How the engine may touch `G` and `G::Curve` in place.  arkworks'
+/// short-Weierstrass `Affine { x, y, infinity: bool }` and `Projective
+/// { x, y, z }` carry no `repr(C)`, so their field order is probed once per
+/// kernel on the curve's generator instead of assumed (the reference reads
+/// `G::Curve` straight out of a device buffer, multiexp.rs:209-211):
+///   * `ark_affine`: x at offset 0, y right after it, the `infinity` flag in
+///     the byte after y, record size 2 coordinates + 8 -- the layout
+///     `ECG_BASES_ARK_AFFINE` reads on the device;
+///   * `projective_xyz`: `Projective::from(generator)` is the bytes of
+///     [x | y | one], i.e. the engine's Jacobian [X, Y, Z] result can be
+///     written in place.
+#[derive(Clone, Copy, Debug)]
+pub(crate) struct ArkLayout {
+    pub ark_affine: bool,
+    pub projective_xyz: bool,
+}
+
+fn bytes_of<T>(v: &T) -> &[u8] {
+    // only called on field elements and projective points: no padding bytes
+    unsafe { std::slice::from_raw_parts(v as *const T as *const u8, std::mem::size_of::<T>()) }
+}
+
+pub(crate) fn ark_layout<G: GpuCurveAffine>() -> ArkLayout {
+    let lq = std::mem::size_of::<<G as AffineRepr>::BaseField>();
+    let g = G::generator();
+    let (gx, gy) = match g.xy() {
+        Some(xy) => xy,
+        None => return ArkLayout { ark_affine: false, projective_xyz: false },
+    };
+    let at = |p: &G, f: &<G as AffineRepr>::BaseField| f as *const _ as usize - p as *const G as usize;
+    // the flag byte: the identity has it set, the generator clear (read only
+    // once x and y are known to fill the first 2 lq bytes)
+    let flag = |p: &G| unsafe { std::ptr::read((p as *const G as *const u8).add(2 * lq)) };
+    let ark_affine = std::mem::size_of::<G>() == 2 * lq + 8
+        && at(&g, gx) == 0
+        && at(&g, gy) == lq
+        && flag(&g) == 0
+        && flag(&G::zero()) == 1;
+    let p = g.into_group();
+    let one = <<G as AffineRepr>::BaseField as One>::one();
+    let pb = bytes_of(&p);
+    let projective_xyz = pb.len() == 3 * lq
+        && &pb[..lq] == bytes_of(gx)
+        && &pb[lq..2 * lq] == bytes_of(gy)
+        && &pb[2 * lq..] == bytes_of(&one);
+    ArkLayout { ark_affine, projective_xyz }
+}
 
 /// Multiexp on one device.
 pub struct SingleMultiexpKernel<'a, G>
@@ -25,6 +86,7 @@ where G: GpuCurveAffine
     /// multiexp.rs:71-93).
     n: usize,
     curve: i32,
+    layout: ArkLayout,
     maybe_abort: Option<&'a (dyn Fn() -> bool + Send + Sync)>,
     _phantom: std::marker::PhantomData<G::Scalar>,
 }
@@ -41,28 +103,68 @@ where G: GpuCurveAffine + GpuName
         let curve = curve_id::<G>()?;
         let mut n = 0usize;
         check(unsafe { sys::ecg_msm_chunk_size(program.ctx(), curve, &mut n) })?;
+        let layout = ark_layout::<G>();
+        if !layout.ark_affine {
+            warn!("arkworks Affine is not laid out as {{x, y, infinity}}: bases go over in their GPU form");
+        }
         info!("Multiexp on {} ({} GB, {} CUs): {} terms per pass", device.name(),
               device.memory() >> 30, device.compute_units(), n);
-        Ok(SingleMultiexpKernel { program, n, curve, maybe_abort, _phantom: std::marker::PhantomData })
+        Ok(SingleMultiexpKernel { program, n, curve, layout, maybe_abort, _phantom: std::marker::PhantomData })
     }
 
-    /// sum_i exponents[i] * bases[i].  Bases go over in their GPU form
-    /// ([x, y], identity all zero, as multiexp.rs:152 builds it); exponents are
-    /// canonical `BigInt`s; any length (the engine splits into passes).
+    /// sum_i exponents[i] * bases[i].  The arkworks records are read on the
+    /// device (no host `to_gpu_repr` pass); exponents are canonical `BigInt`s;
+    /// any length (the engine splits into passes).
     pub fn multiexp(
         &self, bases: &[G], exponents: &[<G::Scalar as PrimeField>::Repr],
     ) -> EcResult<G::Curve> {
+        self.multiexp_cached(bases, exponents, false)
+    }
+
+    /// `multiexp`, with `cache` asking the engine to keep these bases resident
+    /// (keyed by address and length) for later calls on the same array.
+    fn multiexp_cached(
+        &self, bases: &[G], exponents: &[<G::Scalar as PrimeField>::Repr], cache: bool,
+    ) -> EcResult<G::Curve> {
         assert_eq!(bases.len(), exponents.len());
         require(&self.program, sys::ECG_KIND_MULTIEXP, self.curve)?;
-        let repr: Vec<_> = bases.iter().map(GpuRepr::to_gpu_repr).collect();
-        let mut acc = G::Curve::zero();
+        if !self.layout.projective_xyz {
+            return Err(EcError::Simple("arkworks Projective is not laid out as [x, y, z]; \
+                                        the engine's result cannot be written into G::Curve"));
+        }
+        let words = std::mem::size_of::<G::Curve>() / 8;
+        let mut out = vec![0u64; words];
         let (cb, user) = abort_hook(&self.maybe_abort);
-        check(unsafe {
-            sys::ecg_msm(self.program.ctx(), self.curve, repr.as_ptr() as *const u64,
-                         exponents.as_ptr() as *const u64, exponents.len(),
-                         &mut acc as *mut G::Curve as *mut u64, cb, user)
-        })?;
+        let rc = if self.layout.ark_affine {
+            unsafe {
+                sys::ecg_msm_ex(self.program.ctx(), self.curve, bases.as_ptr() as *const c_void,
+                                sys::ECG_BASES_ARK_AFFINE, bases.len(), 0, exponents.as_ptr() as *const u64, 0,
+                                exponents.len(), std::ptr::null(), cache as c_int, out.as_mut_ptr(), cb, user)
+            }
+        } else {
+            // the reference's own host conversion (multiexp.rs:152-153)
+            let repr: Vec<_> = bases.iter().map(GpuRepr::to_gpu_repr).collect();
+            unsafe {
+                sys::ecg_msm(self.program.ctx(), self.curve, repr.as_ptr() as *const u64,
+                             exponents.as_ptr() as *const u64, exponents.len(), out.as_mut_ptr(), cb, user)
+            }
+        };
+        check(rc)?;
+        let mut acc = G::Curve::zero();
+        // layout checked by ark_layout: [X | Y | Z], every bit pattern of the
+        // limbs a valid field element (the engine returns them fully reduced)
+        unsafe {
+            std::ptr::copy_nonoverlapping(out.as_ptr() as *const u8, &mut acc as *mut G::Curve as *mut u8,
+                                          std::mem::size_of::<G::Curve>());
+        }
         Ok(acc)
+    }
+
+    /// Host addresses of the base arrays this kernel's context keeps resident.
+    fn cached_keys(&self) -> Vec<usize> {
+        let mut keys = [std::ptr::null::<c_void>(); 8];
+        let n = unsafe { sys::ecg_base_cache_keys(self.program.ctx(), keys.as_mut_ptr(), keys.len()) };
+        keys[..n.min(keys.len())].iter().map(|&p| p as usize).collect()
     }
 }
 
@@ -71,6 +173,9 @@ pub struct MultiexpKernel<'a, G>
 where G: GpuCurveAffine
 {
     kernels: Vec<SingleMultiexpKernel<'a, G>>,
+    /// Base arrays the engine's caches hold on device (keyed by address):
+    /// kept alive while any context caches a range of them.
+    pinned: Vec<Arc<Vec<G>>>,
 }
 
 impl<'a, G> MultiexpKernel<'a, G>
@@ -106,7 +211,7 @@ where G: GpuCurveAffine + GpuName
             return Err(EcError::Simple("No working GPUs found!"));
         }
         info!("Multiexp: {} MI355X context(s)", kernels.len());
-        Ok(MultiexpKernel { kernels })
+        Ok(MultiexpKernel { kernels, pinned: Vec::new() })
     }
 
     /// Device d sums the d-th of ceil(n / #devices)-term ranges, in passes of
@@ -118,12 +223,21 @@ where G: GpuCurveAffine + GpuName
         exps: &'s [<G::Scalar as PrimeField>::Repr],
         results: &'s mut [G::Curve], error: Arc<RwLock<EcResult<()>>>,
     ) {
-        let per_device = (exps.len() + self.kernels.len() - 1) / self.kernels.len().max(1);
+        // borrowed slices of unknown lifetime: never cached
+        Self::split(&self.kernels, scope, bases, exps, results, error, false)
+    }
+
+    fn split<'s>(
+        kernels: &'s [SingleMultiexpKernel<'a, G>], scope: &Scope<'s>, bases: &'s [G],
+        exps: &'s [<G::Scalar as PrimeField>::Repr], results: &'s mut [G::Curve],
+        error: Arc<RwLock<EcResult<()>>>, cache: bool,
+    ) {
+        let per_device = (exps.len() + kernels.len() - 1) / kernels.len().max(1);
         if per_device == 0 {
             return;
         }
         let ranges = bases.chunks(per_device).zip(exps.chunks(per_device));
-        for ((kern, (bs, es)), slot) in self.kernels.iter_mut().zip(ranges).zip(results.iter_mut()) {
+        for ((kern, (bs, es)), slot) in kernels.iter().zip(ranges).zip(results.iter_mut()) {
             let error = error.clone();
             scope.execute(move || {
                 let mut partial = G::Curve::zero();
@@ -131,7 +245,7 @@ where G: GpuCurveAffine + GpuName
                     if error.read().unwrap().is_err() {
                         return;
                     }
-                    match kern.multiexp(b, e) {
+                    match kern.multiexp_cached(b, e, cache) {
                         Ok(p) => partial += p,
                         Err(err) => {
                             *error.write().unwrap() = Err(err);
@@ -147,7 +261,8 @@ where G: GpuCurveAffine + GpuName
     }
 
     /// sum over i of exps[i] * bases_arc[skip + i] across every device; the
-    /// per-device partials are added on the host (multiexp.rs:372-400).
+    /// per-device partials are added on the host (multiexp.rs:372-400).  The
+    /// bases stay resident on the devices for the next call with this `Arc`.
     pub fn multiexp(
         &mut self, pool: &Worker, bases_arc: Arc<Vec<G>>,
         exps: Arc<Vec<<G::Scalar as PrimeField>::Repr>>, skip: usize,
@@ -156,9 +271,26 @@ where G: GpuCurveAffine + GpuName
         let exps = &exps[..];
         let mut partials = vec![G::Curve::zero(); self.kernels.len()];
         let error = Arc::new(RwLock::new(Ok(())));
-        pool.scoped(|s| self.parallel_multiexp(s, bases, exps, &mut partials, error.clone()));
+        let kernels = &self.kernels;
+        pool.scoped(|s| Self::split(kernels, s, bases, exps, &mut partials, error.clone(), true));
+        if !self.pinned.iter().any(|a| Arc::ptr_eq(a, &bases_arc)) {
+            self.pinned.push(bases_arc.clone());
+        }
+        self.release_uncached();
         Arc::try_unwrap(error).expect("only one ref left").into_inner().unwrap()?;
         Ok(partials.into_iter().fold(G::Curve::zero(), |acc, p| acc + p))
+    }
+
+    /// Drop the pinned arrays no context caches any more (the engine keeps
+    /// at most 8 entries per context and evicts the oldest).
+    fn release_uncached(&mut self) {
+        let keys: Vec<usize> = self.kernels.iter().flat_map(|k| k.cached_keys()).collect();
+        let size = std::mem::size_of::<G>();
+        self.pinned.retain(|a| {
+            let lo = a.as_ptr() as usize;
+            let hi = lo + a.len() * size;
+            keys.iter().any(|&k| k >= lo && k < hi)
+        });
     }
 
     /// Kernels (devices) in use.

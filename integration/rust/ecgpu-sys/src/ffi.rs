@@ -50,6 +50,17 @@ pub const ECG_SORT_PW_BLOCK: c_int = 2;
 /// multiexp.rs:140-144).
 pub type ecg_abort_cb = Option<unsafe extern "C" fn(user: *mut c_void) -> c_int>;
 
+// ---- host transport ops (ecg_comm_init_host) -----------------------------------
+pub const ECG_XCHG_ALLGATHER: c_int = 0;
+pub const ECG_XCHG_ALLTOALL: c_int = 1;
+
+/// `typedef int (*ecg_xchg_cb)(int op, const void *send, void *recv, size_t
+/// bytes, void *user)`: the launcher's group moves the exchange bytes
+/// (host memory) instead of RCCL; returns 0 on success.
+pub type ecg_xchg_cb =
+    Option<unsafe extern "C" fn(op: c_int, send: *const c_void, recv: *mut c_void, bytes: usize,
+                                user: *mut c_void) -> c_int>;
+
 /// Opaque `ecg_ctx`: one device, one stream, a grow-only workspace, a lock.
 #[repr(C)]
 pub struct ecg_ctx {
@@ -135,13 +146,20 @@ extern "C" {
     pub fn ecg_comm_unique_id(out: *mut u8) -> c_int;
     pub fn ecg_comm_init(ctx: *mut ecg_ctx, nranks: c_int, rank: c_int, unique_id: *const u8) -> c_int;
     pub fn ecg_comm_destroy(ctx: *mut ecg_ctx);
+    pub fn ecg_comm_set_timeout(ctx: *mut ecg_ctx, ms: u32) -> c_int;
+    pub fn ecg_comm_init_host(ctx: *mut ecg_ctx, nranks: c_int, rank: c_int, xchg: ecg_xchg_cb,
+                              user: *mut c_void) -> c_int;
     pub fn ecg_comm_allgather(ctx: *mut ecg_ctx, d_send: *const c_void, d_recv: *mut c_void, bytes: usize) -> c_int;
     pub fn ecg_comm_alltoall(ctx: *mut ecg_ctx, d_send: *const c_void, d_recv: *mut c_void,
                              bytes_per_peer: usize) -> c_int;
     pub fn ecg_msm_dist(ctx: *mut ecg_ctx, curve_id: c_int, d_bases: *const c_void, d_scalars: *const c_void,
                         n_local: usize, out_jac: *mut u64) -> c_int;
+    pub fn ecg_msm_dist_ex(ctx: *mut ecg_ctx, curve_id: c_int, d_bases: *const c_void, d_scalars: *const c_void,
+                           n_local: usize, out_jac: *mut u64, abort_cb: ecg_abort_cb, user: *mut c_void) -> c_int;
     pub fn ecg_fft_dist(ctx: *mut ecg_ctx, field_id: c_int, d_local: *mut c_void, omega: *const u64,
                         log_n: u32) -> c_int;
+    pub fn ecg_fft_dist_ex(ctx: *mut ecg_ctx, field_id: c_int, d_local: *mut c_void, omega: *const u64,
+                           log_n: u32, abort_cb: ecg_abort_cb, user: *mut c_void) -> c_int;
     pub fn ecg_fft_dist_stage1(ctx: *mut ecg_ctx, field_id: c_int, d_in: *const c_void, d_out: *mut c_void,
                                omega: *const u64, nranks: u32, rank: u32, log_n: u32) -> c_int;
     pub fn ecg_fft_dist_stage3(ctx: *mut ecg_ctx, d_in: *const c_void, d_out: *mut c_void, nranks: u32,

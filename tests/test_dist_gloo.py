@@ -127,9 +127,13 @@ class _FakeBuf:
         self.ptr = None
 
 
-def _install_device_fakes(rank, world, corrupt=False):
+def _install_device_fakes(rank, world, corrupt=False, fail_rank=None):
     """Swap ecgpu's device entry points for CPU-oracle stand-ins (checker-grade
-    results, so bench.main()'s own checks can pass or fail for real)."""
+    results, so bench.main()'s own checks can pass or fail for real).
+    msm_dist follows ecg_msm_dist_ex's protocol (comm.cpp): every rank
+    all-gathers a [status, partial] record, and any failed status -- here
+    rank `fail_rank` emulating a local allocation failure -- raises the lowest
+    failing rank's error on EVERY rank instead of leaving peers waiting."""
     import coracle as co
     import ecgpu
     from ecgpu import dist as edist
@@ -149,10 +153,21 @@ def _install_device_fakes(rank, world, corrupt=False):
         return co.multiexp_cpu(cid, bases.arr.reshape(-1, 2 * nq)[:n], scal.arr.reshape(-1, 4)[:n],
                                nthreads=2).reshape(-1)
 
-    def msm_dist(prog, curve, bases, scal, n_local):
+    def msm_dist(prog, curve, bases, scal, n_local, maybe_abort=None):
         cid = ecgpu._curve(curve)
-        parts = side.allgather(msm_local(curve, bases, scal, n_local))
-        return _fold(co, cid, parts)
+        if rank == fail_rank:
+            rec = [ecgpu.ECG_ERR_NOMEM, None]
+        elif maybe_abort is not None and maybe_abort():
+            rec = [ecgpu.ECG_ABORTED, None]
+        else:
+            rec = [ecgpu.ECG_OK, msm_local(curve, bases, scal, n_local)]
+        recs = side.allgather(rec)
+        for r, (rc, _) in enumerate(recs):
+            if rc != ecgpu.ECG_OK:
+                if rc == ecgpu.ECG_ABORTED:
+                    raise ecgpu.Aborted("GPU call was aborted!")
+                raise ecgpu.EcError(f"msm_dist: ecg_msm_dist: rank {r} of {world} failed (rc={rc}); every rank stops")
+        return _fold(co, cid, [p for _, p in recs])
 
     def fft_dev(prog, field, d, omega, log_n):
         d.arr[...] = co.serial_fft(fid_of[field], d.arr.reshape(-1, 4), np.asarray(omega, np.uint64), log_n)
@@ -173,13 +188,14 @@ def _install_device_fakes(rank, world, corrupt=False):
     ecgpu.prepare_bases = lambda prog, curve, d, n, window_table=None: d
     ecgpu.msm_dev = lambda prog, curve, b, s, n: msm_local(curve, b, s, n)
     ecgpu.fft_dev = fft_dev
-    edist.comm_init = lambda prog, r, w, bcast: real_comm_init(None, r, w, bcast, make_id=lambda: bytes(range(128)))
+    edist.comm_init = lambda prog, r, w, bcast, **kw: real_comm_init(None, r, w, bcast,
+                                                                     make_id=lambda: bytes(range(128)))
     edist.msm_dist = msm_dist
     edist.fft_dist = fft_dist
     return side
 
 
-def _bench_main_worker(rank, world, port, q, corrupt=False):
+def _bench_main_worker(rank, world, port, q, corrupt=False, fail_rank=None):
     import contextlib
     import io
 
@@ -189,8 +205,9 @@ def _bench_main_worker(rank, world, port, q, corrupt=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     sys.path.insert(0, os.path.join(ROOT, "0g-ec-gpu_amd"))
-    side = _install_device_fakes(rank, world, corrupt)
+    side = _install_device_fakes(rank, world, corrupt, fail_rank)
     import bench
+    import ecgpu
 
     sys.argv = ["bench.py", "--gpus", str(world), "--steps", "2", "--warmup", "1", "--msm-log", "10",
                 "--ntt-log", "8"]
@@ -198,6 +215,10 @@ def _bench_main_worker(rank, world, port, q, corrupt=False):
     try:
         with contextlib.redirect_stdout(out):
             bench.main()
+    except ecgpu.EcError as e:  # the failure reached this rank: report it and exit non-zero
+        q.put((rank, "ERROR " + str(e) + "\n" + out.getvalue()))
+        side.close()
+        sys.exit(3)
     finally:
         side.close()
     q.put((rank, out.getvalue()))
@@ -229,6 +250,31 @@ def test_bench_main_world2(corrupt):
                               "ntt_dist_2gpu_vs_parallel_fft_2^8": not corrupt}
     assert line["value"] > 0 and line["ntt_dist"]["value"] > 0
     assert line["msm_window_table"]["equals_headline_result"] is True
+
+
+@pytest.mark.timeout(300)
+def test_bench_main_world2_failing_rank():
+    """bench.main() at N = 2 with rank 1's distributed MSM failing locally
+    (an emulated allocation failure inside ecg_msm_dist): the status rides in
+    the all-gather, so BOTH ranks raise at that call -- nobody is left in the
+    exchange, both processes exit non-zero well within the timeout, and rank 0
+    prints no JSON line."""
+    import multiprocessing as mp
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_main_worker, args=(r, 2, port, q, False, 1)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert not any(p.is_alive() for p in procs), "a rank hung after its peer failed"
+    outs = dict(q.get(timeout=10) for _ in range(2))
+    assert [p.exitcode for p in procs] == [3, 3]
+    assert outs[0].startswith("ERROR") and "rank 1 of 2 failed" in outs[0]
+    assert outs[1].startswith("ERROR") and "rank 1 of 2 failed" in outs[1]
+    assert '"metric"' not in outs[0]
 
 
 def test_kat_scalar_regeneration_matches_single_rank():

@@ -196,6 +196,27 @@ def test_prepared_registry_across_contexts_and_views(prog):
         raw_view.ptr = None
         assert same(cid, out, want)
     d_raw.free()
+    # the same, with a reused allocation that starts AT the old records address
+    # (the old header address is then outside it, or unmapped): the lookup must
+    # not read the header there, and the address reads as raw bases
+    pb3 = ecgpu.prepare_bases(prog, cname, d_b, n)
+    ptr3 = pb3.ptr.value
+    prog.synchronize()
+    assert hip.hipFree(ctypes.c_void_p(ptr3 - hdr)) == 0
+    pb3.ptr = None
+    held = []
+    for size in (n * 96, n * 128 + hdr, n * 96 + 4096):
+        d = ecgpu.DeviceBuffer(prog, size)
+        held.append(d)
+        if d.ptr.value == ptr3:
+            d.write(B)
+            out = np.zeros(18, np.uint64)
+            ecgpu._check(ecgpu.lib().ecg_msm_dev(prog.handle, cid, d.ptr, d_e.ptr, n,
+                                                 out.ctypes.data_as(ctypes.c_void_p), 0, None))
+            assert same(cid, out, want)
+            break
+    for d in held:
+        d.free()
     for buf in (d_b, d_e, d_e2):
         buf.free()
     other.close()

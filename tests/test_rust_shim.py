@@ -74,7 +74,7 @@ def _split_args(s):
 
 def _c_kind(decl):
     """'ptr', 'int' (32-bit int / enum-like), 'u32', 'usize', 'void', 'fnptr'."""
-    if "ecg_abort_cb" in decl:
+    if "ecg_abort_cb" in decl or "ecg_xchg_cb" in decl:
         return "fnptr"
     if "*" in decl:
         return "ptr"
@@ -93,7 +93,7 @@ def _c_kind(decl):
 
 def _rs_kind(ty):
     ty = ty.strip()
-    if ty == "ecg_abort_cb":
+    if ty in ("ecg_abort_cb", "ecg_xchg_cb"):
         return "fnptr"
     if ty.startswith("*"):
         return "ptr"
@@ -222,3 +222,60 @@ def test_parser_sees_a_drifted_signature():
     assert drifted != src
     want = json.load(open(API))["modules"]["ec_gpu_proxy::multiexp"]["methods"]["MultiexpKernel::create"]
     assert rs.parse(drifted)["methods"]["MultiexpKernel::create"]["params"] != want["params"]
+
+
+def _call_args(src, name):
+    """Argument lists of every `sys::<name>(...)` call in src."""
+    out = []
+    for m in re.finditer(r"\bsys::%s\(" % name, src):
+        depth, i = 1, m.end()
+        while depth:
+            depth += {"(": 1, ")": -1}.get(src[i], 0)
+            i += 1
+        out.append([" ".join(a.split()) for a in _split_args(src[m.end():i - 1])])
+    return out
+
+
+def _fn_body(src, header):
+    """Text of the fn whose signature starts with `header`, up to its closing brace."""
+    i = src.index(header)
+    i = src.index("{", i)
+    depth, j = 1, i + 1
+    while depth:
+        depth += {"{": 1, "}": -1}.get(src[j], 0)
+        j += 1
+    return src[i:j]
+
+
+def test_multiexp_reads_ark_affine_on_device_and_caches_arc_bases():
+    """The drop-in's MSM path: arkworks Affine records go
+    to ecg_msm_ex as they are (ECG_BASES_ARK_AFFINE, converted on the device;
+    no host to_gpu_repr Vec except the probed-layout fallback), with the
+    cache flag set exactly on MultiexpKernel::multiexp's Arc-held bases (not on
+    borrowed slices); cached arrays are pinned while the engine caches them;
+    the result is written only after the Projective layout probe passed."""
+    src = open(os.path.join(RUST, "ec-gpu-proxy/src/amd/multiexp.rs")).read()
+    calls = _call_args(src, "ecg_msm_ex")
+    assert len(calls) == 1
+    args = calls[0]
+    assert args[3] == "sys::ECG_BASES_ARK_AFFINE" and args[9] == "std::ptr::null()"
+    assert args[10] == "cache as c_int"
+    assert src.count("GpuRepr::to_gpu_repr") == 1  # only the fallback for an unexpected Affine layout
+    fallback = _fn_body(src, "fn multiexp_cached(")
+    assert "if self.layout.ark_affine" in fallback and "to_gpu_repr" in fallback.split("} else {", 1)[1]
+    assert "if !self.layout.projective_xyz" in fallback
+    # cache flag: true for the Arc path, false for borrowed slices
+    assert "Self::split(kernels, s, bases, exps, &mut partials, error.clone(), true)" in _fn_body(src, "pub fn multiexp(\n        &mut self")
+    assert "Self::split(&self.kernels, scope, bases, exps, results, error, false)" in _fn_body(src, "pub fn parallel_multiexp<'s>(")
+    assert "self.multiexp_cached(bases, exponents, false)" in _fn_body(src, "pub fn multiexp(\n        &self")
+    # pinning follows the engine's cache keys
+    assert "ecg_base_cache_keys" in src and "self.pinned.push(bases_arc.clone())" in src
+    assert "fn ark_layout<G: GpuCurveAffine>()" in src
+
+
+def test_ag_cuda_ec_upload_has_table_form_and_true_size():
+    src = open(os.path.join(RUST, "ag-cuda-ec/src/multiexp.rs")).read()
+    assert "pub fn upload_multiexp_bases_table(" in src
+    assert "pub fn upload_multiexp_bases_table_st(" in src and "pub fn upload_multiexp_bases_table_mt(" in src
+    assert len(_call_args(src, "ecg_msm_prepare_table")) == 1
+    assert "stride * repr.len()" in src  # DeviceData::size is the device buffer's size
