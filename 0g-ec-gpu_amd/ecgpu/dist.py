@@ -41,12 +41,24 @@ class HostGroup:
 
     Wire format: length-prefixed JSON frames (None / bool / int / float / str /
     bytes / lists / str-keyed dicts) -- nothing received is ever unpickled or
-    executed.  A peer joins by answering rank 0's random challenge with
-    HMAC-SHA256(key, challenge || rank); the key is ECGPU_HOSTGROUP_KEY if set,
-    else derived from the launch (TORCHELASTIC_RUN_ID and MASTER_PORT, which
-    every rank of one launch shares).  Rank 0 drops connections that fail the
-    handshake, name an out-of-range or duplicate rank, or stall, and keeps
-    accepting until every rank has joined or `timeout` expires."""
+    executed.
+
+    Authentication is mutual and covers every frame.  Rank 0 sends a random
+    challenge c0; the joining peer answers with its rank, its own challenge c1
+    and HMAC-SHA256(key, "join" | c0 | c1 | rank); rank 0 answers with
+    HMAC(key, "accept" | c0 | c1 | rank), so the peer also knows it reached a
+    holder of the key (not a process that took the port first).  Both derive a
+    session key HMAC(key, "session" | c0 | c1 | rank), and every later frame
+    carries HMAC(session, direction | sequence number | payload): a frame that
+    was forged, altered, replayed or reordered is refused (ConnectionError).
+
+    The key is ECGPU_HOSTGROUP_KEY when set.  Without it, a single-node launch
+    (LOCAL_WORLD_SIZE == WORLD_SIZE, rank 0 bound to loopback) derives it from
+    the launch (TORCHELASTIC_RUN_ID and the port); a multi-node launch, whose
+    rank 0 listens on MASTER_ADDR, refuses to start without an explicit key
+    (fail closed).  Rank 0 drops connections that fail the handshake, name an
+    out-of-range or duplicate rank, or stall, and keeps accepting until every
+    rank has joined or `timeout` expires."""
 
     _MAX_FRAME = 1 << 20
 
@@ -61,6 +73,7 @@ class HostGroup:
         self._conn = None
         self._listener = None
         self._timeout = timeout
+        self._sess: dict = {}   # peer rank (rank 0) or 0 (peers) -> [session key, send seq, recv seq]
         if world == 1:
             return
         self._key = key if key is not None else _launch_key(port)
@@ -98,28 +111,36 @@ class HostGroup:
                         raise
                     time.sleep(0.05)
             c.settimeout(timeout)
-            challenge = _recv_exact(c, 32)
-            c.sendall(rank.to_bytes(4, "little") + _mac(self._key, challenge, rank))
-            if _recv_exact(c, 2) != b"ok":
+            import hmac
+
+            c0 = _recv_exact(c, 32)
+            c1 = os.urandom(32)
+            c.sendall(rank.to_bytes(4, "little") + c1 + _mac(self._key, b"join", c0, c1, rank))
+            reply = _recv_exact(c, 34)
+            if reply[:2] != b"ok" or not hmac.compare_digest(reply[2:], _mac(self._key, b"accept", c0, c1, rank)):
                 c.close()
-                raise ConnectionError("HostGroup: rank 0 refused this rank")
+                raise ConnectionError("HostGroup: rank 0 refused this rank, or could not prove it holds the key")
+            self._sess[0] = [_mac(self._key, b"session", c0, c1, rank), 0, 0]
             self._conn = c
 
     def _admit(self, c, peers: dict):
-        """Challenge one connection; its rank if admitted, else None."""
+        """Mutual handshake with one connection; its rank if admitted, else None."""
         import hmac
         import socket
 
         try:
             c.settimeout(10.0)
-            challenge = os.urandom(32)
-            c.sendall(challenge)
-            msg = _recv_exact(c, 36)
+            c0 = os.urandom(32)
+            c.sendall(c0)
+            msg = _recv_exact(c, 68)
             r = int.from_bytes(msg[:4], "little")
-            if not (1 <= r < self.world) or r in peers or not hmac.compare_digest(msg[4:], _mac(self._key, challenge, r)):
+            c1 = msg[4:36]
+            if not (1 <= r < self.world) or r in peers or not hmac.compare_digest(
+                    msg[36:], _mac(self._key, b"join", c0, c1, r)):
                 return None
-            c.sendall(b"ok")
+            c.sendall(b"ok" + _mac(self._key, b"accept", c0, c1, r))
             c.settimeout(self._timeout)
+            self._sess[r] = [_mac(self._key, b"session", c0, c1, r), 0, 0]
             return r
         except (OSError, socket.timeout, ConnectionError):
             return None
@@ -129,49 +150,69 @@ class HostGroup:
         """RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT as torch.distributed.run
         sets them; the group listens on MASTER_PORT + offset (the launcher's
         own store holds MASTER_PORT).  On a single-node launch (LOCAL_WORLD_SIZE
-        == WORLD_SIZE) rank 0 binds the loopback interface only."""
+        == WORLD_SIZE) rank 0 binds the loopback interface only; a multi-node
+        launch needs ECGPU_HOSTGROUP_KEY (a secret every rank's environment
+        shares) and refuses to start without it."""
         rank = int(os.environ.get("RANK", "0"))
         world = int(os.environ.get("WORLD_SIZE", "1"))
         addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = int(os.environ.get("MASTER_PORT", "29500")) + offset
         single_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+        if world > 1 and not single_node and not os.environ.get("ECGPU_HOSTGROUP_KEY"):
+            raise PermissionError("HostGroup: a multi-node launch listens on MASTER_ADDR, so it needs a secret: "
+                                  "set ECGPU_HOSTGROUP_KEY to the same random value on every rank")
         bind = "127.0.0.1" if single_node else addr
         if single_node:
             addr = "127.0.0.1"
         return HostGroup(rank, world, addr, port, bind_addr=bind)
 
-    # -- framing
-    @staticmethod
-    def _send(c, obj) -> None:
-        data = json.dumps(_enc(obj), separators=(",", ":")).encode()
-        c.sendall(len(data).to_bytes(8, "little") + data)
+    # -- framing: length | payload | HMAC(session, direction | seq | payload)
+    def _send(self, c, peer: int, obj) -> None:
+        import hmac
 
-    def _recv(self, c):
+        sess = self._sess[peer]
+        data = json.dumps(_enc(obj), separators=(",", ":")).encode()
+        tag = hmac.new(sess[0], b"s" + bytes([self.rank == 0]) + sess[1].to_bytes(8, "little") + data,
+                       hashlib.sha256).digest()
+        sess[1] += 1
+        c.sendall(len(data).to_bytes(8, "little") + data + tag)
+
+    def _recv(self, c, peer: int):
+        import hmac
+
+        sess = self._sess[peer]
         n = int.from_bytes(_recv_exact(c, 8), "little")
         if n > self._MAX_FRAME:
             raise ConnectionError(f"HostGroup: frame of {n} bytes exceeds {self._MAX_FRAME}")
-        return _dec(json.loads(_recv_exact(c, n)))
+        data = _recv_exact(c, n)
+        tag = _recv_exact(c, 32)
+        want = hmac.new(sess[0], b"s" + bytes([self.rank != 0]) + sess[2].to_bytes(8, "little") + data,
+                        hashlib.sha256).digest()
+        if not hmac.compare_digest(tag, want):
+            raise ConnectionError("HostGroup: a frame failed authentication (forged, altered or replayed)")
+        sess[2] += 1
+        return _dec(json.loads(data))
 
     def allgather(self, obj: Any) -> list:
         if self.world == 1:
             return [obj]
         if self.rank == 0:
-            out = [obj] + [self._recv(c) for c in self._peers]
-            for c in self._peers:
-                self._send(c, out)
+            out = [obj] + [self._recv(c, r) for r, c in enumerate(self._peers, 1)]
+            for r, c in enumerate(self._peers, 1):
+                self._send(c, r, out)
             return out
-        self._send(self._conn, obj)
-        return self._recv(self._conn)
+        self._send(self._conn, 0, obj)
+        return self._recv(self._conn, 0)
 
     def broadcast(self, obj: Any = None) -> Any:
         """rank 0's obj on every rank."""
         if self.world == 1:
             return obj
         if self.rank == 0:
-            for c in self._peers:
-                self._send(c, obj)
+            for r, c in enumerate(self._peers, 1):
+                self._send(c, r, obj)
             return obj
-        return self._recv(self._conn)
+        return self._recv(self._conn, 0)
 
     def barrier(self) -> None:
         self.allgather(None)
@@ -197,10 +238,10 @@ def _launch_key(port: int) -> bytes:
     return hashlib.sha256(f"ecgpu-hostgroup|{run}|{port}".encode()).digest()
 
 
-def _mac(key: bytes, challenge: bytes, rank: int) -> bytes:
+def _mac(key: bytes, label: bytes, c0: bytes, c1: bytes, rank: int) -> bytes:
     import hmac
 
-    return hmac.new(key, challenge + rank.to_bytes(4, "little"), hashlib.sha256).digest()
+    return hmac.new(key, label + b"|" + c0 + c1 + rank.to_bytes(4, "little"), hashlib.sha256).digest()
 
 
 def _recv_exact(c, n: int) -> bytes:

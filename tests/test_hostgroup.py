@@ -1,7 +1,10 @@
 """HostGroup (ecgpu.dist): the N>1 launch's control channel (RCCL id,
 barriers, max over ranks).  Checks the wire format carries plain values only,
-that rank 0 authenticates peers (challenge + HMAC) and survives bad or
-duplicate joiners, and that a missing broadcast is a clear error."""
+that the handshake is mutual (rank 0 authenticates peers and proves the key
+back, so an impostor rank 0 is refused), that every frame is authenticated
+(a tampered or replayed frame is refused), that rank 0 survives bad or
+duplicate joiners, that a multi-node launch without a key fails closed, and
+that a missing broadcast is a clear error."""
 import os
 import socket
 import sys
@@ -70,7 +73,8 @@ def test_hostgroup_rejects_bad_and_duplicate_peers():
             except OSError:
                 pass
         ch = edist._recv_exact(c, 32)
-        c.sendall(claim.to_bytes(4, "little") + edist._mac(k, ch, claim))
+        c1 = os.urandom(32)
+        c.sendall(claim.to_bytes(4, "little") + c1 + edist._mac(k, b"join", ch, c1, claim))
         assert c.recv(2) == b""  # closed without "ok"
         c.close()
     t1 = threading.Thread(target=_rank, args=(1, 3, port, out, key))
@@ -94,7 +98,8 @@ def test_hostgroup_duplicate_rank_refused():
 
         def client():
             ch = edist._recv_exact(b, 32)
-            b.sendall((1).to_bytes(4, "little") + edist._mac(g._key, ch, 1))
+            c1 = os.urandom(32)
+            b.sendall((1).to_bytes(4, "little") + c1 + edist._mac(g._key, b"join", ch, c1, 1))
 
         t = threading.Thread(target=client)
         t.start()
@@ -108,3 +113,78 @@ def test_comm_init_needs_broadcast():
     with pytest.raises(ValueError, match="broadcast"):
         edist.comm_init(None, 1, 2, None, make_id=lambda: bytes(128))
     assert edist.comm_init(None, 0, 1) == bytes(128)
+
+
+def test_peer_refuses_impostor_rank0():
+    """A process that holds the port but not the key cannot pose as rank 0:
+    it cannot produce the accept proof, so the joining rank refuses it."""
+    port = _free_port()
+    ls = socket.socket()
+    ls.bind(("127.0.0.1", port))
+    ls.listen(1)
+
+    def impostor():
+        c, _ = ls.accept()
+        c.sendall(os.urandom(32))
+        edist._recv_exact(c, 68)
+        c.sendall(b"ok" + os.urandom(32))  # no key: a guessed proof
+        c.close()
+
+    t = threading.Thread(target=impostor)
+    t.start()
+    with pytest.raises(ConnectionError, match="prove"):
+        edist.HostGroup(1, 2, "127.0.0.1", port, key=b"k" * 32, timeout=10)
+    t.join(10)
+    ls.close()
+
+
+def test_frames_are_authenticated():
+    """Frames after the handshake carry a session MAC with a sequence number:
+    a flipped byte, or a frame replayed, is refused."""
+    port = _free_port()
+    key = b"f" * 32
+    holder = {}
+
+    def r0():
+        holder[0] = edist.HostGroup(0, 2, "127.0.0.1", port, key=key, timeout=20)
+
+    t = threading.Thread(target=r0)
+    t.start()
+    g1 = edist.HostGroup(1, 2, "127.0.0.1", port, key=key, timeout=20)
+    t.join(20)
+    g0 = holder[0]
+    try:
+        # a genuine frame goes through
+        g1._send(g1._conn, 0, {"v": 1})
+        assert g0._recv(g0._peers[0], 1) == {"v": 1}
+        # capture the next frame on the wire, then deliver it tampered
+        a, b = socket.socketpair()
+        g1._send(a, 0, [7, 8])
+        raw = edist._recv_exact(b, 8 + len(b"[7,8]") + 32)
+        tampered = raw[:8] + b"[7,9]" + raw[8 + 5:]
+        c, d = socket.socketpair()
+        c.sendall(tampered)
+        with pytest.raises(ConnectionError, match="authentication"):
+            g0._recv(d, 1)
+        # the genuine frame, delivered twice: the replay fails (sequence number)
+        e, f = socket.socketpair()
+        e.sendall(raw + raw)
+        # (the refused tampered copy consumed no sequence number)
+        assert g0._recv(f, 1) == [7, 8]
+        with pytest.raises(ConnectionError, match="authentication"):
+            g0._recv(f, 1)
+        for sck in (a, b, c, d, e, f):
+            sck.close()
+    finally:
+        g1.close()
+        g0.close()
+
+
+def test_multinode_launch_without_key_fails_closed(monkeypatch):
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setenv("WORLD_SIZE", "16")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setenv("MASTER_ADDR", "10.0.0.1")
+    monkeypatch.delenv("ECGPU_HOSTGROUP_KEY", raising=False)
+    with pytest.raises(PermissionError, match="ECGPU_HOSTGROUP_KEY"):
+        edist.HostGroup.from_env()
