@@ -47,6 +47,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "ctx.hpp"
@@ -787,6 +788,59 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
   if (t == 0) store_xyzz(&out[blockIdx.x], pts.get(0));
 }
 
+// 6b. Segment offsets by bits (one-task MSMs).  The offsets of step 5 are
+//     sum_s (s LS) R_s = LS sum_k 2^k T_k,  T_k = sum_{s : bit k of s set} R_s,
+//     k < KB = ceil(log2 S): KB plain tree sums, no point doubling on the
+//     device; the host applies LS 2^k while it folds the windows
+//     (msm_host_fold_bits).  Where msm_reduce_offset_kernel ran a double-and-
+//     add of ~log2(B) dependent doublings per segment (latency-bound below
+//     2^23: 0.58 ms of a 2^20 MSM; 28 point ops per segment at 2^26), the bit
+//     sums cost KB S / 2 adds in trees of depth ~log2(S).  One launch also sums
+//     A = sum_s A_s: group g = w (KB + 1) + k sums T_k of window w for k < KB,
+//     and A for k = KB.  T_k's i-th input is segment
+//     ((i >> k) << (k + 1)) | 2^k | (i mod 2^k), i < 2^(KB-1) (those >= S are
+//     the identity).  Workgroup b of a group sums inputs [b 2 256, (b+1) 2 256).
+template <class F>
+__global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
+    msm_offset_bits_kernel(const XYZZ<F>* __restrict__ partial, const XYZZ<F>* __restrict__ runs, uint32_t S,
+                           uint32_t KB, uint32_t wgs, XYZZ<F>* __restrict__ out) {
+  extern __shared__ uint32_t lds_pts[];
+  const LdsPoints<F> pts{lds_pts};
+  const uint32_t g = blockIdx.x / wgs, b = blockIdx.x % wgs, t = threadIdx.x;
+  const uint32_t w = g / (KB + 1), k = g % (KB + 1);
+  const bool a_sum = k == KB;
+  const XYZZ<F>* src = (a_sum ? partial : runs) + (size_t)w * S;
+  const uint32_t cnt = a_sum ? S : (1u << (KB - 1));
+  const uint32_t span = MSM_THREADS * MSM_TREE_K;
+  const uint32_t j0 = (b * MSM_THREADS + t) * MSM_TREE_K;
+  XYZZ<F> acc = xyzz_zero<F>();
+#pragma unroll 1
+  for (uint32_t q = 0; q < MSM_TREE_K; q++) {
+    const uint32_t i = j0 + q;
+    if (i >= cnt) break;
+    const uint32_t sg = a_sum ? i : (((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1)));
+    if (sg < S) acc = pa_add(acc, load_xyzz(&src[sg]));
+  }
+  pts.put(t, acc);
+  __syncthreads();
+  const uint32_t left = cnt > b * span ? cnt - b * span : 0;
+  const uint32_t active = left >= span ? MSM_THREADS : (left + MSM_TREE_K - 1) / MSM_TREE_K;
+  uint32_t top = 1;
+  while (top < active) top <<= 1;
+#pragma unroll 1
+  for (uint32_t stride = top / 2; stride > 0; stride >>= 1) {
+    if (t < stride) pts.put(t, pa_add(pts.get(t), pts.get(t + stride)));
+    __syncthreads();
+  }
+  if (t == 0) store_xyzz(&out[blockIdx.x], pts.get(0));
+}
+
+static uint32_t offset_bits(uint32_t S) {  // KB of msm_offset_bits_kernel
+  uint32_t kb = 0;
+  while ((1u << kb) < S) kb++;
+  return kb;
+}
+
 // A few points per group (batched MSMs: 2 reduction segments per (task,
 // window)): one thread per group adds them serially.  A tree-sum workgroup per
 // group would run 8 LDS levels of adds for 2 inputs (13.9 ms on the AMT shape,
@@ -1041,6 +1095,9 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   using X = XYZZ<F>;
   MsmPlan pl = pl0;  // reduction segments sized for this point form's occupancy
   plan_reduction(pl, RedWaves<F>::value);
+  // one-task MSMs leave per window the A sum and the KB offset-bit sums
+  // (msm_offset_bits_kernel, folded on the host); batched ones the window sums
+  const bool bits = folded == nullptr;
   const size_t m = (size_t)g.n_chunks * g.clen;  // scalars consumed
   const uint32_t nb = pl.G * pl.B;
   const uint32_t sentinel = nb;
@@ -1166,18 +1223,38 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   hipLaunchKernelGGL(msm_reduce_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
                      dim3(MSM_THREADS), 0, s, (const X*)bk, pl, (X*)pa, (X*)runs);
   ECG_HIP(hipGetLastError());
-  hipLaunchKernelGGL(msm_reduce_offset_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
-                     dim3(MSM_THREADS), 0, s, (const X*)runs, pl, (X*)pa);
-  ECG_HIP(hipGetLastError());
-
   uint32_t cnt = pl.S;
+  uint32_t groups = pl.G;
   X* in = (X*)pa;
   X* out = (X*)pb;
   const size_t tree_lds = (size_t)LdsPoints<F>::NW * MSM_THREADS * 4;
-  if (tree_lds > 64 * 1024)  // G2 points (96 KiB per workgroup) need the opt-in
+  if (tree_lds > 64 * 1024) {  // G2 points (96 KiB per workgroup) need the opt-in
     ECG_HIP(hipFuncSetAttribute((const void*)msm_tree_sum_kernel<F>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)tree_lds));
-  if (cnt > 1 && cnt <= MSM_GROUP_SERIAL) {
+    ECG_HIP(hipFuncSetAttribute((const void*)msm_offset_bits_kernel<F>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)tree_lds));
+  }
+  if (bits) {
+    const uint32_t kb = offset_bits(pl.S);
+    const uint32_t wgs = (pl.S + tree_span - 1) / tree_span;
+    groups = pl.G * (kb + 1);
+    void* pbits;
+    ECG_TRY(ws_get(ctx, "msm_pbits", (size_t)groups * wgs * sizeof(X), &pbits));
+    hipLaunchKernelGGL(msm_offset_bits_kernel<F>, dim3(groups * wgs), dim3(MSM_THREADS), tree_lds, s, (const X*)pa,
+                       (const X*)runs, pl.S, kb, wgs, (X*)pbits);
+    ECG_HIP(hipGetLastError());
+    in = (X*)pbits;
+    cnt = wgs;
+    void* pb2;
+    ECG_TRY(ws_get(ctx, "msm_pbits2", ((size_t)groups * ((wgs + tree_span - 1) / tree_span) + groups) * sizeof(X),
+                   &pb2));
+    out = (X*)pb2;
+  } else {
+    hipLaunchKernelGGL(msm_reduce_offset_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
+                       dim3(MSM_THREADS), 0, s, (const X*)runs, pl, (X*)pa);
+    ECG_HIP(hipGetLastError());
+  }
+  if (!bits && cnt > 1 && cnt <= MSM_GROUP_SERIAL) {
     hipLaunchKernelGGL(msm_group_sum_kernel<F>, dim3(blocks_for(pl.G, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
                        (const X*)in, cnt, pl.G, out);
     ECG_HIP(hipGetLastError());
@@ -1186,8 +1263,8 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   }
   while (cnt > 1) {
     const uint32_t wgs = (cnt + tree_span - 1) / tree_span;
-    hipLaunchKernelGGL(msm_tree_sum_kernel<F>, dim3(pl.G * wgs), dim3(MSM_THREADS), tree_lds, s, (const X*)in, cnt,
-                       wgs, out);
+    hipLaunchKernelGGL(msm_tree_sum_kernel<F>, dim3(groups * wgs), dim3(MSM_THREADS), tree_lds, s, (const X*)in,
+                       cnt, wgs, out);
     ECG_HIP(hipGetLastError());
     X* t = in;
     in = out;
@@ -1207,8 +1284,9 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
       npts = tasks;
       *folded = true;
     }
+    if (bits) npts = groups;
     void* st;
-    ECG_TRY(ws_get(ctx, "msm_sums_std", (size_t)pl.G * sizeof(XYZZ<typename C::Fq>), &st));
+    ECG_TRY(ws_get(ctx, "msm_sums_std", (size_t)npts * sizeof(XYZZ<typename C::Fq>), &st));
     hipLaunchKernelGGL((msm_sums_to_std_kernel<F, typename C::Fq>), dim3(blocks_for(npts, 64)), dim3(64), 0, s,
                        (const X*)in, npts, (XYZZ<typename C::Fq>*)st);
     ECG_HIP(hipGetLastError());
@@ -1401,25 +1479,69 @@ int msm_prepare_t(ecg_ctx* ctx, const void* d_bases, size_t n, uint32_t tab_c, v
   return ECG_ERR_INVALID;
 }
 
-// Horner fold of one pass's W window sums (lazy device XYZZ) into `total`
-// on the host (multiexp.rs:221-233).
+// The plan msm_core_impl runs for a one-task MSM (its reduction segments are
+// sized for the pipeline point form's occupancy), and how many sums it leaves:
+// per window the A sum and offset_bits(S) bit sums (msm_offset_bits_kernel).
 template <class C>
-void msm_host_fold(const XYZZ<typename C::Fq>* win, const MsmPlan& pl, host::HPoint<HostF<C>>& total) {
+MsmPlan msm_eff_plan(MsmPlan pl) {
+  if constexpr (MsmField<C>::rr) {
+    if (msm_rr_enabled()) {
+      plan_reduction(pl, RedWaves<typename MsmField<C>::type>::value);
+      return pl;
+    }
+  }
+  plan_reduction(pl, RedWaves<typename C::Fq>::value);
+  return pl;
+}
+static inline uint32_t msm_single_sums(const MsmPlan& e) { return e.G * (offset_bits(e.S) + 1); }
+
+template <class C>
+host::HPoint<HostF<C>> msm_host_load(const XYZZ<typename C::Fq>& s) {
+  host::HPoint<HostF<C>> p;
+  static_assert(sizeof(p.X) == sizeof(s.X), "host/device coordinate layouts differ");
+  memcpy(&p.X, &s.X, sizeof(p.X));
+  memcpy(&p.Y, &s.Y, sizeof(p.Y));
+  memcpy(&p.ZZ, &s.ZZ, sizeof(p.ZZ));
+  memcpy(&p.ZZZ, &s.ZZZ, sizeof(p.ZZZ));
+  p.X = host::hcanon(p.X);  // device values are in the lazy range [0, 2p]
+  p.Y = host::hcanon(p.Y);
+  p.ZZ = host::hcanon(p.ZZ);
+  p.ZZZ = host::hcanon(p.ZZZ);
+  return p;
+}
+
+// One-task fold of msm_offset_bits_kernel's sums (e = the effective plan):
+// window w's sum is A_w + LS sum_k 2^k T_{w,k} (Horner over the bits, then LS
+// by double-and-add), computed for all windows at once on host threads (each
+// is ~2 KB point ops, independent); then the Horner over windows
+// (multiexp.rs:221-233) adds them into `total`.
+template <class C>
+void msm_host_fold_bits(const XYZZ<typename C::Fq>* sums, const MsmPlan& e, host::HPoint<HostF<C>>& total) {
   using HX = host::HPoint<HostF<C>>;
+  const uint32_t kb = offset_bits(e.S), nw = e.fold_windows();
+  std::vector<HX> win(nw);
+  auto window = [&](uint32_t w) {
+    const XYZZ<typename C::Fq>* g = sums + (size_t)w * (kb + 1);
+    HX x = HX::zero();
+    for (int k = (int)kb - 1; k >= 0; k--) x = host::hadd_pts(host::hdbl(x), msm_host_load<C>(g[k]));
+    HX y = HX::zero();  // LS x
+    for (int b = 31 - __builtin_clz(e.LS); b >= 0; b--) {
+      y = host::hdbl(y);
+      if ((e.LS >> b) & 1) y = host::hadd_pts(y, x);
+    }
+    win[w] = host::hadd_pts(msm_host_load<C>(g[kb]), y);
+  };
+  if (nw >= 4 && kb >= 4) {
+    std::vector<std::thread> th;
+    for (uint32_t w = 0; w < nw; w++) th.emplace_back(window, w);
+    for (auto& t : th) t.join();
+  } else {
+    for (uint32_t w = 0; w < nw; w++) window(w);
+  }
   HX acc = HX::zero();
-  for (int w = (int)pl.fold_windows() - 1; w >= 0; w--) {
-    for (uint32_t k = 0; k < pl.c; k++) acc = host::hdbl(acc);
-    HX ww;
-    static_assert(sizeof(ww.X) == sizeof(win[w].X), "host/device coordinate layouts differ");
-    memcpy(&ww.X, &win[w].X, sizeof(ww.X));
-    memcpy(&ww.Y, &win[w].Y, sizeof(ww.Y));
-    memcpy(&ww.ZZ, &win[w].ZZ, sizeof(ww.ZZ));
-    memcpy(&ww.ZZZ, &win[w].ZZZ, sizeof(ww.ZZZ));
-    ww.X = host::hcanon(ww.X);  // device values are in the lazy range [0, 2p]
-    ww.Y = host::hcanon(ww.Y);
-    ww.ZZ = host::hcanon(ww.ZZ);
-    ww.ZZZ = host::hcanon(ww.ZZZ);
-    acc = host::hadd_pts(acc, ww);
+  for (int w = (int)nw - 1; w >= 0; w--) {
+    for (uint32_t k = 0; k < e.c; k++) acc = host::hdbl(acc);
+    acc = host::hadd_pts(acc, win[w]);
   }
   total = host::hadd_pts(total, acc);
 }
@@ -1476,11 +1598,12 @@ int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_
                                               (bf.tab_c ? pl.W : 1u))
                               : (const void*)((const F*)d_bases + 2 * off);
     ECG_TRY(msm_core_t<C>(ctx, bp, (const uint4*)d_scalars + 2 * off, g, pl, s, &d_sums, prepared));
-    // window sums -> host; Horner fold over windows (multiexp.rs:221-233)
-    win.resize(pl.fold_windows());
+    // window A / offset-bit sums -> host; Horner fold over windows (multiexp.rs:221-233)
+    const MsmPlan e = msm_eff_plan<C>(pl);
+    win.resize(msm_single_sums(e));
     ECG_HIP(hipMemcpyAsync(win.data(), d_sums, win.size() * sizeof(X), hipMemcpyDeviceToHost, s));
     ECG_HIP(hipStreamSynchronize(s));
-    msm_host_fold<C>(win.data(), pl, total_acc);
+    msm_host_fold_bits<C>(win.data(), e, total_acc);
   }
   host::hto_jac_norm(total_acc, out_jac);
   return ECG_OK;
@@ -1529,7 +1652,7 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
     const size_t m = std::min(pass, n - k * pass);
     plans[k] = bf.tab_c ? make_tab_plan(1, (uint32_t)C::FrParams::BITS, bf.tab_c, bf.tab_n)
                         : make_plan(m, (uint32_t)C::FrParams::BITS);
-    woff[k + 1] = woff[k] + plans[k].fold_windows();
+    woff[k + 1] = woff[k] + msm_single_sums(msm_eff_plan<C>(plans[k]));
   }
   // bytes per base of the resident buffer (all of its table rows)
   const size_t rstride = msm_base_record_bytes<C>() * (bf.tab_c ? msm_table_windows<C>(bf.tab_c) : 1u);
@@ -1571,7 +1694,7 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
     rc = [&]() -> int {
       ECG_HIP(hipStreamWaitEvent(cs, up[b], 0));
       ECG_TRY(msm_core_t<C>(ctx, bp, is[b], g, plans[k], cs, &d_sums, resident));
-      ECG_HIP(hipMemcpyAsync((X*)sums + woff[k], d_sums, plans[k].fold_windows() * sizeof(X),
+      ECG_HIP(hipMemcpyAsync((X*)sums + woff[k], d_sums, (woff[k + 1] - woff[k]) * sizeof(X),
                              hipMemcpyDeviceToDevice, cs));
       ECG_HIP(hipEventRecord(done[b], cs));
       if (k + 1 < np) {
@@ -1598,7 +1721,7 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
   }
   if (rc != ECG_OK) return rc;
   HX total = HX::zero();
-  for (size_t k = 0; k < np; k++) msm_host_fold<C>(win.data() + woff[k], plans[k], total);
+  for (size_t k = 0; k < np; k++) msm_host_fold_bits<C>(win.data() + woff[k], msm_eff_plan<C>(plans[k]), total);
   host::hto_jac_norm(total, out_jac);
   return ECG_OK;
 }
