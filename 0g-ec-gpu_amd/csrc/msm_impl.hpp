@@ -47,11 +47,11 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
-#include <thread>
 #include <vector>
 
 #include "ctx.hpp"
 #include "curve.hpp"
+#include "host_pool.hpp"
 #include "curve_rr2.hpp"
 #include "dispatch.hpp"
 #include "host_field.hpp"
@@ -557,7 +557,11 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_ACC_ATTR
 //     profiles/r03f/combine_short_ab.txt), so large MSMs keep the levels.
 constexpr uint32_t MSM_SHORT_RUN = 16;
 constexpr uint32_t MSM_SHORT_SEG = 4;
-constexpr size_t MSM_SHORT_MAX_RECS = (size_t)1 << 21;
+constexpr size_t MSM_SHORT_MAX_RECS_DEFAULT_LOG = 21;
+static size_t msm_short_max_recs() {  // A/B: ECG_MSM_SHORT_LOG
+  static const size_t v = (size_t)1 << env_u32("ECG_MSM_SHORT_LOG", MSM_SHORT_MAX_RECS_DEFAULT_LOG);
+  return v;
+}
 template <class F>
 __global__ void __launch_bounds__(MSM_THREADS)
     msm_combine_short_kernel(const XYZZ<F>* __restrict__ rin, const uint32_t* __restrict__ kin, size_t n,
@@ -691,10 +695,13 @@ struct LdsPoint {  // XYZZ<F> words of lane t at w[i * MSM_THREADS + t]
   }
 };
 
+// Several bucket arrays (slots, `slot_stride` buckets apart) hold the buckets
+// of the passes of one MSM (msm_host_t): bucket j is their sum, added into the
+// running sum slot by slot -- one reduction for every pass.
 template <class F>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
     msm_reduce_kernel(const XYZZ<F>* __restrict__ buckets, MsmPlan pl, XYZZ<F>* __restrict__ partial,
-                      XYZZ<F>* __restrict__ runs) {
+                      XYZZ<F>* __restrict__ runs, uint32_t slots, size_t slot_stride) {
   __shared__ uint32_t lds[LdsPoint<F>::NW * MSM_THREADS];
   const LdsPoint<F> acc_l{lds};
   const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
@@ -705,7 +712,8 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
   XYZZ<F> run = xyzz_zero<F>();
   acc_l.put(xyzz_zero<F>());
   for (int j = (int)len - 1; j >= 0; j--) {
-    run = pa_add(run, load_xyzz(&bk[j]));
+#pragma unroll 1
+    for (uint32_t q = 0; q < slots; q++) run = pa_add(run, load_xyzz(&bk[q * slot_stride + j]));
     acc_l.put(pa_add(acc_l.get(), run));
   }
   // acc = sum_j (j+1) S_j ; run = sum_j S_j
@@ -799,11 +807,15 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
 //     A = sum_s A_s: group g = w (KB + 1) + k sums T_k of window w for k < KB,
 //     and A for k = KB.  T_k's i-th input is segment
 //     ((i >> k) << (k + 1)) | 2^k | (i mod 2^k), i < 2^(KB-1) (those >= S are
-//     the identity).  Workgroup b of a group sums inputs [b 2 256, (b+1) 2 256).
+//     the identity).  Workgroup b of a group sums inputs [b 256 K, (b+1) 256 K),
+//     K serially per thread, then log2(256) LDS levels.  Every add here waits
+//     for the previous one (~20 us for a full add at this occupancy), so K is
+//     chosen (offset_bits_k) to fit all the workgroups in ONE round of the
+//     CUs: 16 + 1 dependent adds at 2^20-2^23 where K = 2 took 4 rounds of 10.
 template <class F>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
     msm_offset_bits_kernel(const XYZZ<F>* __restrict__ partial, const XYZZ<F>* __restrict__ runs, uint32_t S,
-                           uint32_t KB, uint32_t wgs, XYZZ<F>* __restrict__ out) {
+                           uint32_t KB, uint32_t K, uint32_t wgs, XYZZ<F>* __restrict__ out) {
   extern __shared__ uint32_t lds_pts[];
   const LdsPoints<F> pts{lds_pts};
   const uint32_t g = blockIdx.x / wgs, b = blockIdx.x % wgs, t = threadIdx.x;
@@ -811,11 +823,15 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
   const bool a_sum = k == KB;
   const XYZZ<F>* src = (a_sum ? partial : runs) + (size_t)w * S;
   const uint32_t cnt = a_sum ? S : (1u << (KB - 1));
-  const uint32_t span = MSM_THREADS * MSM_TREE_K;
-  const uint32_t j0 = (b * MSM_THREADS + t) * MSM_TREE_K;
+  const uint32_t span = MSM_THREADS * K;
+  if (b * span >= cnt) {  // this group has fewer inputs than the widest one: the identity
+    if (t == 0) store_xyzz(&out[blockIdx.x], xyzz_zero<F>());
+    return;
+  }
+  const uint32_t j0 = (b * MSM_THREADS + t) * K;
   XYZZ<F> acc = xyzz_zero<F>();
 #pragma unroll 1
-  for (uint32_t q = 0; q < MSM_TREE_K; q++) {
+  for (uint32_t q = 0; q < K; q++) {
     const uint32_t i = j0 + q;
     if (i >= cnt) break;
     const uint32_t sg = a_sum ? i : (((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1)));
@@ -823,8 +839,8 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
   }
   pts.put(t, acc);
   __syncthreads();
-  const uint32_t left = cnt > b * span ? cnt - b * span : 0;
-  const uint32_t active = left >= span ? MSM_THREADS : (left + MSM_TREE_K - 1) / MSM_TREE_K;
+  const uint32_t left = cnt - b * span;
+  const uint32_t active = left >= span ? MSM_THREADS : (left + K - 1) / K;
   uint32_t top = 1;
   while (top < active) top <<= 1;
 #pragma unroll 1
@@ -839,6 +855,23 @@ static uint32_t offset_bits(uint32_t S) {  // KB of msm_offset_bits_kernel
   uint32_t kb = 0;
   while ((1u << kb) < S) kb++;
   return kb;
+}
+
+// Inputs per thread of msm_offset_bits_kernel: the smallest power of two
+// (>= 2, <= 32) whose non-empty workgroups fit one round of 2 per CU (its LDS
+// use), so the launch is one tree's latency (A/B: ECG_MSM_BITS_K pins it).
+static uint32_t offset_bits_k(uint32_t G, uint32_t S, uint32_t cus) {
+  const uint32_t pinned = env_u32("ECG_MSM_BITS_K", 0);
+  if (pinned) return pinned;
+  const uint32_t kb = offset_bits(S);
+  uint32_t K = 2;
+  for (; K < 32; K *= 2) {
+    const uint32_t span = MSM_THREADS * K;
+    const uint64_t real = (uint64_t)G * ((S + span - 1) / span) +
+                          (kb ? (uint64_t)G * kb * (((1u << (kb - 1)) + span - 1) / span) : 0);
+    if (real <= 2ull * cus) break;
+  }
+  return K;
 }
 
 // A few points per group (batched MSMs: 2 reduction segments per (task,
@@ -1088,9 +1121,22 @@ int msm_plan_info_t(size_t n, uint32_t window_bits, uint32_t* c, uint32_t* windo
 // reduced-radix form, whose bases are converted first).
 // prepared: d_bases already holds the pipeline's base records
 // (msm_prepare_t), so the per-call conversion is skipped.
+// Phases of msm_core_impl: steps 1-4 (digits, sort, accumulation, combine)
+// into bucket slot `slot`, and steps 5-6 (reduction over `slots` bucket
+// slots, offsets, trees).  A pipelined MSM (msm_host_t) runs the first for
+// each pass into its own slot and the second once.
+// CORE_RESERVE only sizes the workspace (for the largest pass, before a
+// pipeline starts: a buffer grown mid-pipeline would stall it).
+enum MsmCorePhase { CORE_ALL = 0, CORE_ACC = 1, CORE_FIN = 2, CORE_RESERVE = 3 };
+struct MsmSlots {
+  uint32_t slot = 0;   // CORE_ACC: the bucket slot this pass fills (< slots)
+  uint32_t slots = 1;  // the MSM's bucket slots (CORE_FIN reduces them all)
+};
+
 template <class C, class AF>
 int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g,
-                  const MsmPlan& pl0, hipStream_t s, void** d_sums, bool prepared, bool* folded) {
+                  const MsmPlan& pl0, hipStream_t s, void** d_sums, bool prepared, bool* folded,
+                  MsmCorePhase phase = CORE_ALL, MsmSlots sl = MsmSlots{}) {
   using F = AF;
   using X = XYZZ<F>;
   MsmPlan pl = pl0;  // reduction segments sized for this point form's occupancy
@@ -1098,6 +1144,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   // one-task MSMs leave per window the A sum and the KB offset-bit sums
   // (msm_offset_bits_kernel, folded on the host); batched ones the window sums
   const bool bits = folded == nullptr;
+  const bool do_acc = phase == CORE_ALL || phase == CORE_ACC, do_fin = phase == CORE_ALL || phase == CORE_FIN;
   const size_t m = (size_t)g.n_chunks * g.clen;  // scalars consumed
   const uint32_t nb = pl.G * pl.B;
   const uint32_t sentinel = nb;
@@ -1116,25 +1163,57 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   const size_t nseg_all = nseg * g.n_lines;                 // accumulation threads (all lines)
 
   void *e0, *e1, *bk, *rc, *rk, *rc2, *rk2, *pa, *pb, *tmp;
+  // the bucket slots, then one word: the long-run flag of msm_combine_short_kernel
+  // every phase asks for all the MSM's slots: the grow-only workspace is
+  // sized once, so slots filled by earlier passes are never reallocated
+  const uint32_t nslots = sl.slots;
+  ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nslots * nb * sizeof(X) + 256, &bk));
+  X* const bk_all = (X*)bk;
+  uint32_t* long_runs = (uint32_t*)((char*)bk + (size_t)nslots * nb * sizeof(X));
+  if (phase == CORE_ACC) {
+    // this pass's slot; the flag word sits after the last slot in use
+    bk = (void*)(bk_all + (size_t)sl.slot * nb);
+    long_runs = (uint32_t*)((char*)bk_all + (size_t)nslots * nb * sizeof(X));
+  }
+  ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
+  const uint32_t tree_span = MSM_TREE_K * MSM_THREADS;  // inputs per tree-sum workgroup
+  ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * ((pl.S + tree_span - 1) / tree_span) + pl.G) * sizeof(X), &pb));
+  // sort geometry (section 2 below)
+  uint32_t wbits = 0;
+  while ((1u << wbits) < line_groups) wbits++;
+  const bool pw_one = sort_mode == ECG_SORT_PW_ONE;
+  const int cfg = pw ? msm_sort_cfg() : 0;
+  const size_t sort_n = pw && !pw_one ? mpad : total;  // one sort per block, or one sort of all blocks
+  const int sort_bits = pw ? (int)(pw_one ? pl.c + wbits : pl.c) : key_bits;
+  if (do_acc || phase == CORE_RESERVE) {
   ECG_TRY(ws_get(ctx, "msm_e0", total * 8, &e0));
   ECG_TRY(ws_get(ctx, "msm_e1", total * 8, &e1));
-  // the buckets, then one word: the long-run flag of msm_combine_short_kernel
-  ECG_TRY(ws_get(ctx, "msm_buckets", (size_t)nb * sizeof(X) + 256, &bk));
-  uint32_t* long_runs = (uint32_t*)((char*)bk + (size_t)nb * sizeof(X));
   ECG_TRY(ws_get(ctx, "msm_recs", 2 * nseg_all * sizeof(X), &rc));
   ECG_TRY(ws_get(ctx, "msm_rkeys", 2 * nseg_all * 4, &rk));
   const uint32_t comb_seg = msm_combine_seg();
   const size_t nseg1 = (2 * nseg_all + comb_seg - 1) / comb_seg;
   ECG_TRY(ws_get(ctx, "msm_recs2", 2 * nseg1 * sizeof(X), &rc2));
   ECG_TRY(ws_get(ctx, "msm_rkeys2", 2 * nseg1 * 4, &rk2));
-  ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
-  const uint32_t tree_span = MSM_TREE_K * MSM_THREADS;  // inputs per tree-sum workgroup
-  ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * ((pl.S + tree_span - 1) / tree_span) + pl.G) * sizeof(X), &pb));
+  size_t tmp_bytes = 0;
+  ECG_HIP(msm_sort(cfg, nullptr, tmp_bytes, (uint64_t*)e0, (uint64_t*)e1, sort_n, 0, sort_bits, s));
+  ECG_TRY(ws_get(ctx, "msm_sort_tmp", tmp_bytes, &tmp));
+  if (msm_short_runs() && 2 * nseg_all < msm_short_max_recs()) {
+    void* ks;
+    ECG_TRY(ws_get(ctx, "msm_rkeys_short", 2 * nseg_all * 4, &ks));
+  }
+  if constexpr (!std::is_same<F, typename C::Fq>::value) {
+    if (!prepared) {
+      void* rb;
+      ECG_TRY(ws_get(ctx, "msm_rr_bases", (size_t)g.n_lines * g.line_len * BaseLayout<F>::BYTES, &rb));
+    }
+  }
+  if (phase == CORE_RESERVE) return ECG_OK;
 
   // buckets nobody writes (no term) stay the identity: all-zero XYZZ (ZZ = 0).
   // (Running this clear and the base conversion on a side stream, concurrent
   // with the digits and the sorts, measured no gain: all are HBM-bound.)
-  ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X) + 4, s));
+  ECG_HIP(hipMemsetAsync(bk, 0, (size_t)nb * sizeof(X), s));
+  ECG_HIP(hipMemsetAsync(long_runs, 0, 4, s));
   const F* bases = (const F*)d_bases;
   if constexpr (!std::is_same<F, typename C::Fq>::value) {
     const size_t nb_in = (size_t)g.n_lines * g.line_len;  // every base a value can index
@@ -1163,15 +1242,6 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   // where it was and yields exactly the per-block result.  Per-block sorts
   // of <= 2^22 entries took rocPRIM's small-input path (10 launches per block
   // at 2^20: 2.7 of the 7.1 ms MSM) or onesweep launch tails.
-  uint32_t wbits = 0;
-  while ((1u << wbits) < line_groups) wbits++;
-  const bool pw_one = sort_mode == ECG_SORT_PW_ONE;
-  const int cfg = pw ? msm_sort_cfg() : 0;
-  const size_t sort_n = pw && !pw_one ? mpad : total;  // one sort per block, or one sort of all blocks
-  const int sort_bits = pw ? (int)(pw_one ? pl.c + wbits : pl.c) : key_bits;
-  size_t tmp_bytes = 0;
-  ECG_HIP(msm_sort(cfg, nullptr, tmp_bytes, (uint64_t*)e0, (uint64_t*)e1, sort_n, 0, sort_bits, s));
-  ECG_TRY(ws_get(ctx, "msm_sort_tmp", tmp_bytes, &tmp));
   for (size_t o = 0; o < total; o += sort_n)
     ECG_HIP(msm_sort(cfg, tmp, tmp_bytes, (uint64_t*)e0 + o, (uint64_t*)e1 + o, sort_n, 0, sort_bits, s));
 
@@ -1195,7 +1265,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   X* rout = (X*)rc2;
   uint32_t* kout = (uint32_t*)rk2;
   const uint32_t* lflag = nullptr;
-  if (msm_short_runs() && nrec < MSM_SHORT_MAX_RECS) {
+  if (msm_short_runs() && nrec < msm_short_max_recs()) {
     void* ks;
     ECG_TRY(ws_get(ctx, "msm_rkeys_short", nrec * 4, &ks));
     hipLaunchKernelGGL(msm_combine_short_kernel<F>,
@@ -1217,11 +1287,13 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     std::swap(rin, rout);
     std::swap(kin, kout);
   }
+  }  // do_acc
+  if (!do_fin) return ECG_OK;
 
   void* runs;
   ECG_TRY(ws_get(ctx, "msm_runs", (size_t)pl.G * pl.S * sizeof(X), &runs));
   hipLaunchKernelGGL(msm_reduce_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
-                     dim3(MSM_THREADS), 0, s, (const X*)bk, pl, (X*)pa, (X*)runs);
+                     dim3(MSM_THREADS), 0, s, (const X*)bk_all, pl, (X*)pa, (X*)runs, nslots, (size_t)nb);
   ECG_HIP(hipGetLastError());
   uint32_t cnt = pl.S;
   uint32_t groups = pl.G;
@@ -1236,12 +1308,13 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   }
   if (bits) {
     const uint32_t kb = offset_bits(pl.S);
-    const uint32_t wgs = (pl.S + tree_span - 1) / tree_span;
+    const uint32_t K = offset_bits_k(pl.G, pl.S, (uint32_t)ctx->compute_units);
+    const uint32_t wgs = (pl.S + MSM_THREADS * K - 1) / (MSM_THREADS * K);
     groups = pl.G * (kb + 1);
     void* pbits;
     ECG_TRY(ws_get(ctx, "msm_pbits", (size_t)groups * wgs * sizeof(X), &pbits));
     hipLaunchKernelGGL(msm_offset_bits_kernel<F>, dim3(groups * wgs), dim3(MSM_THREADS), tree_lds, s, (const X*)pa,
-                       (const X*)runs, pl.S, kb, wgs, (X*)pbits);
+                       (const X*)runs, pl.S, kb, K, wgs, (X*)pbits);
     ECG_HIP(hipGetLastError());
     in = (X*)pbits;
     cnt = wgs;
@@ -1301,14 +1374,15 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
 // per task and sets *folded.
 template <class C>
 int msm_core_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const MsmGeom& g, const MsmPlan& pl,
-               hipStream_t s, void** d_sums, bool prepared = false, bool* folded = nullptr) {
+               hipStream_t s, void** d_sums, bool prepared = false, bool* folded = nullptr,
+               MsmCorePhase phase = CORE_ALL, MsmSlots sl = MsmSlots{}) {
   if (folded) *folded = false;
   if constexpr (MsmField<C>::rr) {
     if (msm_rr_enabled())
       return msm_core_impl<C, typename MsmField<C>::type>(ctx, d_bases, d_scalars, g, pl, s, d_sums, prepared,
-                                                          folded);
+                                                          folded, phase, sl);
   }
-  return msm_core_impl<C, typename C::Fq>(ctx, d_bases, d_scalars, g, pl, s, d_sums, prepared, nullptr);
+  return msm_core_impl<C, typename C::Fq>(ctx, d_bases, d_scalars, g, pl, s, d_sums, prepared, nullptr, phase, sl);
 }
 
 // Bytes per base in the pipeline's own layout: 128-B reduced-radix records
@@ -1512,8 +1586,8 @@ host::HPoint<HostF<C>> msm_host_load(const XYZZ<typename C::Fq>& s) {
 
 // One-task fold of msm_offset_bits_kernel's sums (e = the effective plan):
 // window w's sum is A_w + LS sum_k 2^k T_{w,k} (Horner over the bits, then LS
-// by double-and-add), computed for all windows at once on host threads (each
-// is ~2 KB point ops, independent); then the Horner over windows
+// by double-and-add), computed for all windows at once on the host pool's
+// threads (each is ~30 independent point ops); then the Horner over windows
 // (multiexp.rs:221-233) adds them into `total`.
 template <class C>
 void msm_host_fold_bits(const XYZZ<typename C::Fq>* sums, const MsmPlan& e, host::HPoint<HostF<C>>& total) {
@@ -1531,13 +1605,10 @@ void msm_host_fold_bits(const XYZZ<typename C::Fq>* sums, const MsmPlan& e, host
     }
     win[w] = host::hadd_pts(msm_host_load<C>(g[kb]), y);
   };
-  if (nw >= 4 && kb >= 4) {
-    std::vector<std::thread> th;
-    for (uint32_t w = 0; w < nw; w++) th.emplace_back(window, w);
-    for (auto& t : th) t.join();
-  } else {
+  if (nw >= 4 && kb >= 4)
+    HostPool::get().parallel_for(nw, [&](size_t w) { window((uint32_t)w); });
+  else
     for (uint32_t w = 0; w < nw; w++) window(w);
-  }
   HX acc = HX::zero();
   for (int w = (int)nw - 1; w >= 0; w--) {
     for (uint32_t k = 0; k < e.c; k++) acc = host::hdbl(acc);
@@ -1621,12 +1692,17 @@ static uint32_t msm_h2d_passes() {  // host-slice pipeline depth (A/B: ECG_MSM_H
 // passes whose upload overlaps the previous pass's compute: pass k+1's bases
 // and scalars go H2D on a copy stream into the other half of a double-
 // buffered staging area while the compute stream runs pass k (the
-// accumulation is VALU-bound, the copy is PCIe-bound).  Each pass leaves its
-// W window sums in a device array; one D2H and the host Horner folds follow
-// the last pass.  Same group element as the single-pass MSM.
+// accumulation is VALU-bound, the copy is PCIe-bound).  Every pass of a batch
+// of up to MSM_MAX_SLOTS passes fills its own bucket slot with one plan for
+// the whole MSM, and ONE reduction sums the slots bucket by bucket
+// (msm_reduce_kernel adds them into its running sums): a pass costs its
+// digits, sort and accumulation, not a reduction of 2^(c-1) W buckets of its
+// own.  Same group element as the single-pass MSM.
 // bf.prepared: `bases` is a device-resident prepared buffer (the base cache of
 // ecg_msm_ex, an Arc<Vec<G>> seen again): only the 32-B scalars travel, and
-// they still overlap the previous pass's compute.
+// the passes grow geometrically (first n / 16, then x2): the first pass's
+// upload is the only one not hidden behind compute.
+constexpr uint32_t MSM_MAX_SLOTS = 8;
 template <class C>
 int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scalars, size_t n, uint32_t scalar_mont,
                uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
@@ -1640,39 +1716,60 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
   }
   const bool resident = bf.prepared;
   const size_t bb = 2 * sizeof(F), sb = 32;
-  size_t pass = msm_pass_terms<C>(ctx);
-  if (n >= ((size_t)1 << 22)) {
-    const size_t want = (n + msm_h2d_passes() - 1) / msm_h2d_passes();
-    if (want < pass) pass = want;
+  // ---- pass sizes
+  const size_t maxpass = msm_pass_terms<C>(ctx);
+  std::vector<size_t> poff{0};
+  if (n >= ((size_t)1 << 22) && resident) {
+    // A/B: ECG_MSM_PASS_FIRST (1/x of n) and ECG_MSM_PASS_GROWTH
+    static const uint32_t first_div = std::max(1u, env_u32("ECG_MSM_PASS_FIRST", 16));
+    static const uint32_t growth = std::max(2u, env_u32("ECG_MSM_PASS_GROWTH", 2));
+    size_t m = std::max<size_t>((n / first_div + 255) / 256 * 256, 1);
+    while (poff.back() < n) {
+      const size_t left = n - poff.back();
+      const size_t take = std::min({m, left, maxpass});
+      poff.push_back(poff.back() + (left - take < m / 2 && left <= maxpass ? left : take));  // no tiny last pass
+      m *= growth;
+    }
+  } else {
+    size_t pass = maxpass;
+    if (n >= ((size_t)1 << 22)) pass = std::min(pass, (n + msm_h2d_passes() - 1) / msm_h2d_passes());
+    for (size_t o = pass; o < n; o += pass) poff.push_back(o);
+    poff.push_back(n);
   }
-  const size_t np = (n + pass - 1) / pass;
-  std::vector<MsmPlan> plans(np);
-  std::vector<size_t> woff(np + 1, 0);
-  for (size_t k = 0; k < np; k++) {
-    const size_t m = std::min(pass, n - k * pass);
-    plans[k] = bf.tab_c ? make_tab_plan(1, (uint32_t)C::FrParams::BITS, bf.tab_c, bf.tab_n)
-                        : make_plan(m, (uint32_t)C::FrParams::BITS);
-    woff[k + 1] = woff[k] + msm_single_sums(msm_eff_plan<C>(plans[k]));
-  }
+  const size_t np = poff.size() - 1;
+  size_t pmax = 0;
+  for (size_t k = 0; k < np; k++) pmax = std::max(pmax, poff[k + 1] - poff[k]);
+  // one plan for every pass: passes of a batch share its bucket slots
+  const MsmPlan pl = bf.tab_c ? make_tab_plan(1, (uint32_t)C::FrParams::BITS, bf.tab_c, bf.tab_n)
+                              : make_plan(n, (uint32_t)C::FrParams::BITS);
+  const size_t nsums = msm_single_sums(msm_eff_plan<C>(pl));
+  const size_t nbatch = (np + MSM_MAX_SLOTS - 1) / MSM_MAX_SLOTS;
+  const uint32_t slots = (uint32_t)std::min<size_t>(np, MSM_MAX_SLOTS);
   // bytes per base of the resident buffer (all of its table rows)
   const size_t rstride = msm_base_record_bytes<C>() * (bf.tab_c ? msm_table_windows<C>(bf.tab_c) : 1u);
   void *ib[2] = {nullptr, nullptr}, *is[2] = {nullptr, nullptr}, *sums;
-  if (!resident) ECG_TRY(ws_get(ctx, "msm_in_bases", pass * bb, &ib[0]));
-  ECG_TRY(ws_get(ctx, "msm_in_scalars", pass * sb, &is[0]));
+  if (!resident) ECG_TRY(ws_get(ctx, "msm_in_bases", pmax * bb, &ib[0]));
+  ECG_TRY(ws_get(ctx, "msm_in_scalars", pmax * sb, &is[0]));
   if (np > 1) {
-    if (!resident) ECG_TRY(ws_get(ctx, "msm_in_bases_b", pass * bb, &ib[1]));
-    ECG_TRY(ws_get(ctx, "msm_in_scalars_b", pass * sb, &is[1]));
+    if (!resident) ECG_TRY(ws_get(ctx, "msm_in_bases_b", pmax * bb, &ib[1]));
+    ECG_TRY(ws_get(ctx, "msm_in_scalars_b", pmax * sb, &is[1]));
   }
-  ECG_TRY(ws_get(ctx, "msm_pass_sums", woff[np] * sizeof(X), &sums));
+  ECG_TRY(ws_get(ctx, "msm_pass_sums", nbatch * nsums * sizeof(X), &sums));
   if (!ctx->copy_stream) ECG_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
   hipStream_t cs = ctx->stream, us = ctx->copy_stream;
+  {  // every workspace buffer at its largest size before the pipeline starts
+    const MsmGeom g{1, 1, pmax, pmax, scalar_mont};
+    void* unused = nullptr;
+    ECG_TRY(msm_core_t<C>(ctx, bases, is[0], g, pl, cs, &unused, resident, nullptr, CORE_RESERVE,
+                          MsmSlots{0, slots}));
+  }
   hipEvent_t up[2], done[2];
   for (int i = 0; i < 2; i++) {
     ECG_HIP(hipEventCreateWithFlags(&up[i], hipEventDisableTiming));
     ECG_HIP(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
   }
   auto upload = [&](size_t k) -> int {
-    const size_t off = k * pass, m = std::min(pass, n - off);
+    const size_t off = poff[k], m = poff[k + 1] - off;
     const int b = (int)(k & 1);
     if (!resident)
       ECG_HIP(hipMemcpyAsync(ib[b], (const uint8_t*)bases + off * bb, m * bb, hipMemcpyHostToDevice, us));
@@ -1687,28 +1784,34 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
       break;
     }
     const int b = (int)(k & 1);
-    const size_t m = std::min(pass, n - k * pass);
+    const size_t m = poff[k + 1] - poff[k];
     const MsmGeom g{1, 1, m, m, scalar_mont};
-    void* d_sums = nullptr;
-    const void* bp = resident ? (const void*)((const uint8_t*)bases + k * pass * rstride) : ib[b];
+    const size_t batch = k / MSM_MAX_SLOTS;
+    const uint32_t slot = (uint32_t)(k % MSM_MAX_SLOTS);
+    const bool last_of_batch = slot + 1 == MSM_MAX_SLOTS || k + 1 == np;
+    const void* bp = resident ? (const void*)((const uint8_t*)bases + poff[k] * rstride) : ib[b];
     rc = [&]() -> int {
       ECG_HIP(hipStreamWaitEvent(cs, up[b], 0));
-      ECG_TRY(msm_core_t<C>(ctx, bp, is[b], g, plans[k], cs, &d_sums, resident));
-      ECG_HIP(hipMemcpyAsync((X*)sums + woff[k], d_sums, (woff[k + 1] - woff[k]) * sizeof(X),
-                             hipMemcpyDeviceToDevice, cs));
+      void* d_sums = nullptr;
+      ECG_TRY(msm_core_t<C>(ctx, bp, is[b], g, pl, cs, &d_sums, resident, nullptr, CORE_ACC, MsmSlots{slot, slots}));
       ECG_HIP(hipEventRecord(done[b], cs));
       if (k + 1 < np) {
         if (k >= 1) ECG_HIP(hipStreamWaitEvent(us, done[b ^ 1], 0));  // pass k-1 has released its staging half
         ECG_TRY(upload(k + 1));
       }
+      if (last_of_batch) {  // one reduction over the batch's slots
+        ECG_TRY(msm_core_t<C>(ctx, bp, is[b], g, pl, cs, &d_sums, resident, nullptr, CORE_FIN,
+                              MsmSlots{0, slot + 1}));
+        ECG_HIP(hipMemcpyAsync((X*)sums + batch * nsums, d_sums, nsums * sizeof(X), hipMemcpyDeviceToDevice, cs));
+      }
       return ECG_OK;
     }();
   }
   (void)hipStreamSynchronize(us);
-  std::vector<X> win(woff[np]);
+  std::vector<X> win(nbatch * nsums);
   if (rc == ECG_OK) {
     rc = [&]() -> int {
-      ECG_HIP(hipMemcpyAsync(win.data(), sums, woff[np] * sizeof(X), hipMemcpyDeviceToHost, cs));
+      ECG_HIP(hipMemcpyAsync(win.data(), sums, win.size() * sizeof(X), hipMemcpyDeviceToHost, cs));
       ECG_HIP(hipStreamSynchronize(cs));
       return ECG_OK;
     }();
@@ -1721,7 +1824,8 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
   }
   if (rc != ECG_OK) return rc;
   HX total = HX::zero();
-  for (size_t k = 0; k < np; k++) msm_host_fold_bits<C>(win.data() + woff[k], msm_eff_plan<C>(plans[k]), total);
+  const MsmPlan e = msm_eff_plan<C>(pl);
+  for (size_t k = 0; k < nbatch; k++) msm_host_fold_bits<C>(win.data() + k * nsums, e, total);
   host::hto_jac_norm(total, out_jac);
   return ECG_OK;
 }

@@ -472,7 +472,7 @@ def main():
                                            curve=args.curve)
         meta_e = rand_scalars(np.random.default_rng(73), 73, r_int)
         d_re = ecgpu.DeviceBuffer.upload(prog, np.ascontiguousarray(np.resize(meta_e, (nrb, 4))))
-        ecgpu.multiple_multiexp(prog, d_rb, (d_re, nrb), 1024, 8, False, curve=args.curve)
+        out_rb = ecgpu.multiple_multiexp(prog, d_rb, (d_re, nrb), 1024, 8, False, curve=args.curve)
         best_rb = 1e9
         for _ in range(3):
             t_a = time.perf_counter()
@@ -483,6 +483,25 @@ def main():
             "ms": best_rb * 1e3, "terms_per_s": nrb / best_rb,
             "note": "the reference prints this as 'GPU took {}ms' (bases already uploaded here)"}
         d_rb.free()
+        if not args.no_table and cid in (0, 1):
+            # the same call over bases uploaded in the window-table form -- the Rust
+            # upload_multiexp_bases_table(bases, 4096, 0) path (ecg_msm_prepare_table, one bucket set per task)
+            tw_r = ecgpu.lib().ecg_msm_table_window(cid, nrb // 1024)
+            t_a = time.perf_counter()
+            d_rt = ecgpu.upload_multiexp_bases(prog, np.ascontiguousarray(np.resize(meta_b, (nrb, meta_b.shape[1]))),
+                                               curve=args.curve, window_table=tw_r)
+            rt_prep = time.perf_counter() - t_a
+            out_rt = ecgpu.multiple_multiexp(prog, d_rt, (d_re, nrb), 1024, 8, False, curve=args.curve)
+            best_rt = 1e9
+            for _ in range(3):
+                t_a = time.perf_counter()
+                ecgpu.multiple_multiexp(prog, d_rt, (d_re, nrb), 1024, 8, False, curve=args.curve)
+                best_rt = min(best_rt, time.perf_counter() - t_a)
+            aux["reference_multiexp_bench_shape_table"] = {
+                "window": tw_r, "upload_and_prepare_s": rt_prep, "ms": best_rt * 1e3, "terms_per_s": nrb / best_rt,
+                "equal": bool((out_rt == out_rb).all()),
+                "note": "bases uploaded once with their window table (upload_multiexp_bases_table)"}
+            d_rt.free()
         d_re.free()
         # batched multi-line MSM on the ag-cuda-ec AMT shape (benches/amt.rs: LOG_N=10 -> 2^21 x 10 lines)
         L, lines, chunks = 1 << 21, 10, 1 << 10

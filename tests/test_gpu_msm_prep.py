@@ -123,3 +123,50 @@ def test_base_cache_not_stale(kernels, cname, cid):
     with pytest.raises(ecgpu.EcError, match="cache_bases"):
         k.multiexp_ex(buf.astype(np.int64), exps, cache_bases=True)
     k.clear_base_cache()
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_cached_ark_pipelined_2p22(gpu_programs, cname, cid):
+    """The Rust drop-in's MultiexpKernel::multiexp path at a size that takes
+    the pipelined branch (cached bases, >= 2^22 host exponents): arkworks
+    Affine records read on the device, cached as prepared records, then the
+    exponents in geometrically growing passes whose buckets share one
+    reduction.  With skip, identity bases and Montgomery exponents; checked
+    against the resident single-pass MSM and the known answer
+    sum s_i (a + (skip + i) b) G."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    prog = gpu_programs[0][0]
+    r_int = bench.R_BLS if cid == 0 else bench.R_BN
+    lq = ecgpu.CURVE_FQ_LIMBS[cid]
+    skip, n = 777, (1 << 22) + 12345
+    a, b = 1234567, 89101112
+    d_b = ecgpu.gen_bases_dev(prog, cname, a, b, n + skip)
+    xy = d_b.read(shape=(n + skip, 2 * lq))
+    d_b.free()
+    ark = np.zeros((n + skip, 2 * lq + 1), dtype=np.uint64)
+    ark[:, :2 * lq] = xy
+    ident = [skip + 5, skip + n // 2, skip + n - 1]  # identity bases (infinity set) contribute nothing
+    ark[ident, :2 * lq] = 0
+    ark[ident, 2 * lq] = 1
+    xy[ident] = 0
+    E = bench.rand_scalars(np.random.default_rng(cid + 222), n, r_int)
+    k = ecgpu.MultiexpKernel.create([prog], [], cname)
+    k.clear_base_cache()
+    first = k.multiexp_ex(ark, E, skip=skip, ark_affine=True, cache_bases=True)
+    again = k.multiexp_ex(ark, co.to_mont(2 * cid, E), skip=skip, ark_affine=True, cache_bases=True,
+                          exps_montgomery=True)
+    d_xy = ecgpu.DeviceBuffer.upload(prog, np.ascontiguousarray(xy[skip:]))
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    resident = ecgpu.msm_dev(prog, cname, d_xy, d_e, n)
+    assert (first == resident).all() and (again == resident).all()
+    E_kat = E.copy()
+    E_kat[[i - skip for i in ident]] = 0  # identity bases: their terms vanish
+    kat = co.kat_scalar(cid, (a + skip * b) % r_int, b, E_kat, nthreads=16) % r_int
+    assert (co.jac_to_affine(cid, first) == co.jac_to_affine(cid, co.gen_mul(cid, kat))).all()
+    k.clear_base_cache()
+    d_xy.free()
+    d_e.free()
