@@ -809,9 +809,8 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
 //     ((i >> k) << (k + 1)) | 2^k | (i mod 2^k), i < 2^(KB-1) (those >= S are
 //     the identity).  Workgroup b of a group sums inputs [b 256 K, (b+1) 256 K),
 //     K serially per thread, then log2(256) LDS levels.  Every add here waits
-//     for the previous one (~20 us for a full add at this occupancy), so K is
-//     chosen (offset_bits_k) to fit all the workgroups in ONE round of the
-//     CUs: 16 + 1 dependent adds at 2^20-2^23 where K = 2 took 4 rounds of 10.
+//     for the previous one (~15 us for a full add at this occupancy), so the
+//     launch is sized by K (offset_bits_k) to ~one workgroup per CU.
 template <class F>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
     msm_offset_bits_kernel(const XYZZ<F>* __restrict__ partial, const XYZZ<F>* __restrict__ runs, uint32_t S,
@@ -857,21 +856,18 @@ static uint32_t offset_bits(uint32_t S) {  // KB of msm_offset_bits_kernel
   return kb;
 }
 
-// Inputs per thread of msm_offset_bits_kernel: the smallest power of two
-// (>= 2, <= 32) whose non-empty workgroups fit one round of 2 per CU (its LDS
-// use), so the launch is one tree's latency (A/B: ECG_MSM_BITS_K pins it).
-static uint32_t offset_bits_k(uint32_t G, uint32_t S, uint32_t cus) {
+// Inputs per thread of msm_offset_bits_kernel: enough that one workgroup
+// covers a bit group (2^(KB-1) inputs: K = 2^(KB-9)), within [2, 32].  The
+// launch then has ~G (KB + 1) workgroups, under one per CU.  Measured at 2^20
+// (G = 16, S = 4096): K = 2 / 4 / 8 / 16 / 32 -> 0.67 / 0.54 / 0.45 / 0.38 /
+// 0.59 ms for the offset and A sums (profiles/r04/offset_bits_k_ab.txt); the
+// segment offsets and A tree of round 3 took 0.83 ms.  ECG_MSM_BITS_K pins K.
+static uint32_t offset_bits_k(uint32_t S) {
   const uint32_t pinned = env_u32("ECG_MSM_BITS_K", 0);
   if (pinned) return pinned;
   const uint32_t kb = offset_bits(S);
-  uint32_t K = 2;
-  for (; K < 32; K *= 2) {
-    const uint32_t span = MSM_THREADS * K;
-    const uint64_t real = (uint64_t)G * ((S + span - 1) / span) +
-                          (kb ? (uint64_t)G * kb * (((1u << (kb - 1)) + span - 1) / span) : 0);
-    if (real <= 2ull * cus) break;
-  }
-  return K;
+  const uint32_t k = kb > 9 ? 1u << (kb - 9) : 2u;
+  return std::min(32u, std::max(2u, k));
 }
 
 // A few points per group (batched MSMs: 2 reduction segments per (task,
@@ -1308,7 +1304,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   }
   if (bits) {
     const uint32_t kb = offset_bits(pl.S);
-    const uint32_t K = offset_bits_k(pl.G, pl.S, (uint32_t)ctx->compute_units);
+    const uint32_t K = offset_bits_k(pl.S);
     const uint32_t wgs = (pl.S + MSM_THREADS * K - 1) / (MSM_THREADS * K);
     groups = pl.G * (kb + 1);
     void* pbits;
@@ -1722,7 +1718,7 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
   if (n >= ((size_t)1 << 22) && resident) {
     // A/B: ECG_MSM_PASS_FIRST (1/x of n) and ECG_MSM_PASS_GROWTH
     static const uint32_t first_div = std::max(1u, env_u32("ECG_MSM_PASS_FIRST", 16));
-    static const uint32_t growth = std::max(2u, env_u32("ECG_MSM_PASS_GROWTH", 2));
+    static const uint32_t growth = std::max(2u, env_u32("ECG_MSM_PASS_GROWTH", 3));
     size_t m = std::max<size_t>((n / first_div + 255) / 256 * 256, 1);
     while (poff.back() < n) {
       const size_t left = n - poff.back();

@@ -433,13 +433,16 @@ class LocalExchange:
         return exchange
 
 
-def hostgroup_exchange(group: "HostGroup") -> Callable[[int, bytes, int], bytes]:
-    """comm_init_host callable over a HostGroup (small exchanges: its frames
-    are capped at 1 MiB)."""
+def hostgroup_exchange(group: "HostGroup", piece: int = 256 << 10) -> Callable[[int, bytes, int], bytes]:
+    """comm_init_host callable over a HostGroup.  Its frames are capped at
+    1 MiB (hex-encoded), so payloads go in pieces of `piece` bytes, one
+    all-gather each -- meant for the status records and partial points, and
+    for rehearsal-size all-to-alls, not for bulk data."""
     import ecgpu
 
     def exchange(op: int, data: bytes, nbytes: int) -> bytes:
-        blocks = group.allgather(data)
+        parts = [group.allgather(data[o:o + piece]) for o in range(0, max(len(data), 1), piece)]
+        blocks = [b"".join(p[r] for p in parts) for r in range(group.world)]
         if op == ecgpu.XCHG_ALLGATHER:
             return b"".join(blocks)
         r = group.rank

@@ -114,6 +114,12 @@ def parse(argv=None):
     ap.add_argument("--no-aux", action="store_true", help="skip the batched-MSM / EC-FFT side lines (N=1)")
     ap.add_argument("--no-table", action="store_true",
                     help="skip the window-table (fixed-base) MSM leg (ecg_msm_prepare_table)")
+    ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
+                    help="N > 1 exchange: RCCL over xGMI (one GPU per rank), or the host group "
+                         "(ecg_comm_init_host over HostGroup: a rehearsal of the N > 1 path with several "
+                         "ranks on one GPU, which RCCL refuses)")
+    ap.add_argument("--single-device", action="store_true",
+                    help="every rank on GPU 0 (with --transport host: N-rank rehearsal on a one-GPU box)")
     ap.add_argument("--unprepared", action="store_true",
                     help="time the MSM over [x, y] bases (conversion to the kernel layout inside every step)")
     return ap.parse_args(argv)
@@ -213,8 +219,10 @@ def main():
     fr_fid = ecgpu.CURVE_FR_FIELD[cid]
     lq = ecgpu.CURVE_FQ_LIMBS[cid]
     r_int = R_BLS if cid == 0 else R_BN
-    prog = ecgpu.program(ecgpu.Device(local_rank))
-    if world > 1:
+    prog = ecgpu.program(ecgpu.Device(0 if args.single_device else local_rank))
+    if world > 1 and args.transport == "host":
+        edist.comm_init_host(prog, rank, world, edist.hostgroup_exchange(group))
+    elif world > 1:
         edist.comm_init(prog, rank, world, group.broadcast)
     nthreads = cpu_threads(args.cpu_threads)
 
@@ -630,7 +638,9 @@ def main():
                    "(ecg_msm_prepare_bases, upload_multiexp_bases's role)"),
         "config": {"workload": f"{args.curve} G1 MSM 2^{args.msm_log} terms sharded over {world} GPU(s) "
                                f"+ Fr NTT 2^{log_n} per GPU", "msm_terms": n_total, "ntt_log_n": log_n,
-                   "parallelism": f"range-shard x{world} + RCCL all-gather of partials" if world > 1 else "single GPU"},
+                   "parallelism": (f"range-shard x{world} + "
+                                   + ("RCCL" if args.transport == "rccl" else "host-group (rehearsal)")
+                                   + " all-gather of partials") if world > 1 else "single GPU"},
         "msm_ms_unprepared_bases": unprep_ms,
         "msm_window_table": table,
         "roofline": roofline,

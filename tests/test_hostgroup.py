@@ -188,3 +188,36 @@ def test_multinode_launch_without_key_fails_closed(monkeypatch):
     monkeypatch.delenv("ECGPU_HOSTGROUP_KEY", raising=False)
     with pytest.raises(PermissionError, match="ECGPU_HOSTGROUP_KEY"):
         edist.HostGroup.from_env()
+
+
+def test_hostgroup_exchange_allgather_alltoall_in_pieces():
+    """ecgpu.dist.hostgroup_exchange (the host transport of ecg_comm_init_host
+    over a HostGroup): all-gather and all-to-all semantics, with payloads cut
+    into pieces below the frame cap."""
+    import ecgpu
+
+    port = _free_port()
+    world, nb = 3, 1000
+    out = {}
+
+    def rank(r):
+        g = edist.HostGroup(r, world, "127.0.0.1", port, key=b"x" * 32, timeout=30)
+        try:
+            ex = edist.hostgroup_exchange(g, piece=256)  # tiny pieces: many rounds
+            mine = bytes([r]) * nb
+            ag = ex(ecgpu.XCHG_ALLGATHER, mine, nb)
+            send = b"".join(bytes([16 * r + q]) * nb for q in range(world))  # block q -> rank q
+            a2a = ex(ecgpu.XCHG_ALLTOALL, send, nb)
+            out[r] = (ag, a2a)
+        finally:
+            g.close()
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    for r in range(world):
+        ag, a2a = out[r]
+        assert ag == b"".join(bytes([q]) * nb for q in range(world))
+        assert a2a == b"".join(bytes([16 * q + r]) * nb for q in range(world))
