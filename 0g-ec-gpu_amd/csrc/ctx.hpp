@@ -190,9 +190,21 @@ int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_base
 int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac);
 int msm_pass_terms_run(const ecg_ctx* ctx, int curve_id, size_t* out);
 // MSM over host slices, uploads pipelined with compute (msm_host_t)
-// bases_resident: `bases` is a device prepared buffer (only the scalars travel)
+// Cold fill of a base-cache entry inside the pipelined MSM: pass by pass the
+// host bases (ark Affine records or [x, y]) go up with the scalars and are
+// converted on the device into the prepared buffer `dst` (msm_prepared_alloc,
+// n records), which the pass then reads.
+struct MsmFill {
+  const void* h_bases = nullptr;
+  int ark = 0;
+  int curve_id = 0;
+};
+// bases_resident: `bases` is a device prepared buffer (only the scalars travel);
+// with fill, that buffer is filled from fill->h_bases on the way.
 int msm_host_run(ecg_ctx* ctx, int curve_id, const void* bases, int bases_resident, const void* h_scalars, size_t n,
-                 int scalar_mont, uint64_t* out_jac, ecg_abort_cb abort_cb, void* user);
+                 int scalar_mont, uint64_t* out_jac, ecg_abort_cb abort_cb, void* user,
+                 const MsmFill* fill = nullptr);
+int msm_prepared_alloc(ecg_ctx* ctx, int curve_id, size_t n, uint32_t tab_c, void** d_out, hipStream_t s);
 int gen_bases_run(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint64_t* b, size_t n,
                   void* d_out, hipStream_t s);
 

@@ -640,6 +640,38 @@ static uint64_t bases_fingerprint(const void* host, size_t n, size_t rec_bytes) 
   return h;
 }
 
+// Base cache (ecg_msm_ex cache_bases): entries keyed by (host pointer, n,
+// curve, layout) and a fingerprint of sampled records.  A hit returns the
+// entry's prepared buffer; a same-key entry with other content is dropped.
+static void* cache_find(ecg_ctx* ctx, const void* bases, size_t n, int curve_id, int layout, uint64_t fp) {
+  for (size_t k = 0; k < ctx->base_cache.size(); k++) {
+    auto& e = ctx->base_cache[k];
+    if (e.host == bases && e.n == n && e.curve == curve_id && e.layout == layout) {
+      if (e.fingerprint == fp) return e.dev;
+      (void)hipStreamSynchronize(ctx->stream);  // same address, other content: drop the stale entry
+      base_cache_release(e.dev);
+      ctx->base_cache.erase(ctx->base_cache.begin() + k);
+      return nullptr;
+    }
+  }
+  return nullptr;
+}
+
+static void cache_insert(ecg_ctx* ctx, const void* bases, size_t n, int curve_id, int layout, void* dev,
+                         uint64_t fp) {
+  if (ctx->base_cache.size() >= 8) {  // bounded: drop the oldest entry
+    (void)hipStreamSynchronize(ctx->stream);
+    base_cache_release(ctx->base_cache.front().dev);
+    ctx->base_cache.erase(ctx->base_cache.begin());
+  }
+  ctx->base_cache.push_back({bases, n, curve_id, layout, dev, fp});
+}
+
+static size_t host_rec_bytes(int curve_id, int layout) {
+  const size_t lq = fq_limbs64(curve_id);
+  return layout == ECG_BASES_ARK_AFFINE ? (2 * lq + 1) * 8 : 2 * lq * 8;
+}
+
 // Bases on the device for (bases, layout, n).  Uncached: uploaded (and
 // converted from the ark layout) into the workspace slot `slot` as [x, y].
 // Cached: kept as a prepared buffer (msm_prepare_run: the records the bucket
@@ -649,24 +681,14 @@ static int stage_bases(ecg_ctx* ctx, int curve_id, const void* bases, int layout
                        const char* slot, void** d_out) {
   const size_t lq = fq_limbs64(curve_id);
   const size_t xy_bytes = n * 2 * lq * 8;
-  const size_t raw_bytes = layout == ECG_BASES_ARK_AFFINE ? n * (2 * lq + 1) * 8 : xy_bytes;
+  const size_t rec = host_rec_bytes(curve_id, layout);
   hipStream_t s = ctx->stream;
-  const size_t rec = layout == ECG_BASES_ARK_AFFINE ? (2 * lq + 1) * 8 : 2 * lq * 8;
   uint64_t fp = 0;
   if (cache) {
     fp = bases_fingerprint(bases, n, rec);
-    for (size_t k = 0; k < ctx->base_cache.size(); k++) {
-      auto& e = ctx->base_cache[k];
-      if (e.host == bases && e.n == n && e.curve == curve_id && e.layout == layout) {
-        if (e.fingerprint == fp) {
-          *d_out = e.dev;
-          return ECG_OK;
-        }
-        ECG_HIP(hipStreamSynchronize(s));  // same address, other content: drop the stale entry
-        base_cache_release(e.dev);
-        ctx->base_cache.erase(ctx->base_cache.begin() + k);
-        break;
-      }
+    if (void* hit = cache_find(ctx, bases, n, curve_id, layout, fp)) {
+      *d_out = hit;
+      return ECG_OK;
     }
   }
   const char* xy_slot = cache ? "cache_stage_xy" : slot;
@@ -675,8 +697,8 @@ static int stage_bases(ecg_ctx* ctx, int curve_id, const void* bases, int layout
   if (n) {
     if (layout == ECG_BASES_ARK_AFFINE) {
       void* raw;
-      ECG_TRY(ws_get(ctx, "prep_ark_raw", raw_bytes, &raw));
-      ECG_HIP(hipMemcpyAsync(raw, bases, raw_bytes, hipMemcpyHostToDevice, s));
+      ECG_TRY(ws_get(ctx, "prep_ark_raw", n * rec, &raw));
+      ECG_HIP(hipMemcpyAsync(raw, bases, n * rec, hipMemcpyHostToDevice, s));
       ECG_TRY(bases_from_ark(ctx, curve_id, raw, n, xy, s));
     } else {
       ECG_HIP(hipMemcpyAsync(xy, bases, xy_bytes, hipMemcpyHostToDevice, s));
@@ -690,11 +712,7 @@ static int stage_bases(ecg_ctx* ctx, int curve_id, const void* bases, int layout
   ECG_TRY(msm_prepare_run(ctx, curve_id, xy, n, 0, &prep, s));  // synchronises s
   ws_release(ctx, "cache_stage_xy");
   ws_release(ctx, "prep_ark_raw");
-  if (ctx->base_cache.size() >= 8) {  // bounded: drop the oldest entry
-    base_cache_release(ctx->base_cache.front().dev);
-    ctx->base_cache.erase(ctx->base_cache.begin());
-  }
-  ctx->base_cache.push_back({bases, n, curve_id, layout, prep, fp});
+  cache_insert(ctx, bases, n, curve_id, layout, prep, fp);
   *d_out = prep;
   return ECG_OK;
 }
@@ -726,8 +744,23 @@ int ecg_msm_ex(ecg_ctx* ctx, int curve_id, const void* bases, int bases_layout, 
       set_error("Expected more bases from source.");  // multiexp_cpu.rs:55-61
       return ECG_ERR_INVALID;
     }
-    void* d_prep;
-    ECG_TRY(stage_bases(ctx, curve_id, bases, bases_layout, n_bases, 1, nullptr, &d_prep));
+    const uint64_t fp = bases_fingerprint(bases, n_bases, host_rec_bytes(curve_id, bases_layout));
+    void* d_prep = cache_find(ctx, bases, n_bases, curve_id, bases_layout, fp);
+    if (!d_prep && skip == 0 && n_exps == n_bases) {
+      // cold: the entry is filled pass by pass inside the pipelined MSM (the
+      // base uploads overlap the compute instead of preceding it)
+      ECG_TRY(msm_prepared_alloc(ctx, curve_id, n_bases, 0, &d_prep, s));
+      const MsmFill fill{bases, bases_layout == ECG_BASES_ARK_AFFINE, curve_id};
+      int rc = msm_host_run(ctx, curve_id, d_prep, 1, exps, n_exps, exps_montgomery, out_jac, abort_cb, user, &fill);
+      (void)hipStreamSynchronize(s);
+      if (rc != ECG_OK) {
+        msm_prepared_free(d_prep);  // partly filled: never cached
+        return rc;
+      }
+      cache_insert(ctx, bases, n_bases, curve_id, bases_layout, d_prep, fp);
+      return kt_collect(ctx);
+    }
+    if (!d_prep) ECG_TRY(stage_bases(ctx, curve_id, bases, bases_layout, n_bases, 1, nullptr, &d_prep));
     const uint8_t* b0 = (const uint8_t*)d_prep + skip * msm_prepared_stride(curve_id, 0);
     int rc = msm_host_run(ctx, curve_id, b0, 1, exps, n_exps, exps_montgomery, out_jac, abort_cb, user);
     (void)hipStreamSynchronize(s);

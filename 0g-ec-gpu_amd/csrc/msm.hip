@@ -157,6 +157,38 @@ uint32_t msm_table_window_auto(int curve_id, size_t n) {
   return o ? o->table_auto(n) : 0;
 }
 
+// A registered prepared buffer of n bases (plain records) whose records the
+// caller fills on stream s before anything reads them (msm_host_t's cold
+// cache fill); released with msm_prepared_free.
+int msm_prepared_alloc(ecg_ctx* ctx, int curve_id, size_t n, uint32_t tab_c, void** d_out, hipStream_t s) {
+  const MsmOps* o = msm_ops(curve_id, "prepare_bases");
+  if (!o) return ECG_ERR_INVALID;
+  const size_t bytes = o->prepared_bytes(n, tab_c);
+  void* base = nullptr;
+  hipError_t e = hipMalloc(&base, bytes + PREP_HEADER);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("prepare_bases: device allocation of %zu bytes failed: %s", bytes, hipGetErrorString(e));
+    return ECG_ERR_NOMEM;
+  }
+  void* p = (char*)base + PREP_HEADER;
+  const uint64_t nonce = g_prep_seq.fetch_add(0x9E3779B97F4A7C15ull) ^ (uint64_t)(uintptr_t)p;
+  const uint64_t hdr[2] = {PREP_MAGIC, nonce};
+  if (hipMemcpyAsync(base, hdr, sizeof hdr, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    set_error("prepare_bases: %s", hipGetErrorString(hipGetLastError()));
+    (void)hipFree(base);
+    return ECG_ERR_HIP;
+  }
+  const size_t stride = o->record_bytes() * (tab_c ? o->table_windows(tab_c) : 1u);
+  {
+    std::lock_guard<std::mutex> g(g_prep_mu);
+    g_prep[(uintptr_t)p] = PrepEntry{ctx->device, curve_id, n, tab_c, stride, nonce};
+  }
+  *d_out = p;
+  return ECG_OK;
+}
+
 int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, uint32_t tab_c, void** d_out,
                     hipStream_t s) {
   const MsmOps* o = msm_ops(curve_id, "prepare_bases");
@@ -176,31 +208,16 @@ int msm_prepare_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, u
       return ECG_ERR_INVALID;
     }
   }
-  const size_t bytes = o->prepared_bytes(n, tab_c);
-  void* base = nullptr;
-  hipError_t e = hipMalloc(&base, bytes + PREP_HEADER);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    set_error("prepare_bases: device allocation of %zu bytes failed: %s", bytes, hipGetErrorString(e));
-    return ECG_ERR_NOMEM;
-  }
-  void* p = (char*)base + PREP_HEADER;
-  const uint64_t nonce = g_prep_seq.fetch_add(0x9E3779B97F4A7C15ull) ^ (uint64_t)(uintptr_t)p;
-  const uint64_t hdr[2] = {PREP_MAGIC, nonce};
+  void* p = nullptr;
+  ECG_TRY(msm_prepared_alloc(ctx, curve_id, n, tab_c, &p, s));
   int rc = o->prepare(ctx, d_bases, n, tab_c, p, s);
-  if (rc == ECG_OK && (hipMemcpyAsync(base, hdr, sizeof hdr, hipMemcpyHostToDevice, s) != hipSuccess ||
-                       hipStreamSynchronize(s) != hipSuccess)) {
+  if (rc == ECG_OK && hipStreamSynchronize(s) != hipSuccess) {
     set_error("prepare_bases: %s", hipGetErrorString(hipGetLastError()));
     rc = ECG_ERR_HIP;
   }
   if (rc != ECG_OK) {
-    (void)hipFree(base);
+    msm_prepared_free(p);
     return rc;
-  }
-  const size_t stride = o->record_bytes() * (tab_c ? o->table_windows(tab_c) : 1u);
-  {
-    std::lock_guard<std::mutex> g(g_prep_mu);
-    g_prep[(uintptr_t)p] = PrepEntry{ctx->device, curve_id, n, tab_c, stride, nonce};
   }
   *d_out = p;
   return ECG_OK;
@@ -258,7 +275,7 @@ int point_sum_run(ecg_ctx* ctx, int curve_id, const void* d_points, size_t count
 }
 
 int msm_host_run(ecg_ctx* ctx, int curve_id, const void* bases, int bases_resident, const void* h_scalars, size_t n,
-                 int scalar_mont, uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
+                 int scalar_mont, uint64_t* out_jac, ecg_abort_cb abort_cb, void* user, const MsmFill* fill) {
   if (n > 0x7fffffffull) {
     set_error("multiexp: at most 2^31-1 terms per call");
     return ECG_ERR_INVALID;
@@ -273,7 +290,11 @@ int msm_host_run(ecg_ctx* ctx, int curve_id, const void* bases, int bases_reside
       return ECG_ERR_INVALID;
     }
   }
-  return o->host(ctx, bases, bf, h_scalars, n, scalar_mont ? 1u : 0u, out_jac, abort_cb, user);
+  if (fill && (!bf.prepared || bf.tab_c)) {
+    set_error("multiexp: a cache fill needs a plain prepared buffer");
+    return ECG_ERR_INVALID;
+  }
+  return o->host(ctx, bases, bf, h_scalars, n, scalar_mont ? 1u : 0u, out_jac, abort_cb, user, fill);
 }
 
 int msm_pass_terms_run(const ecg_ctx* ctx, int curve_id, size_t* out) {

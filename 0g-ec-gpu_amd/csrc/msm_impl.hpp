@@ -1699,9 +1699,14 @@ static uint32_t msm_h2d_passes() {  // host-slice pipeline depth (A/B: ECG_MSM_H
 // the passes grow geometrically (first n / 16, then x2): the first pass's
 // upload is the only one not hidden behind compute.
 constexpr uint32_t MSM_MAX_SLOTS = 8;
+// fill (a cache miss of ecg_msm_ex, msm_prepared_alloc'd `bases`): the host
+// bases of each pass go up with its scalars (104 B ark records or 96 B [x, y])
+// and become the buffer's records on the device before the pass reads them;
+// the copies dominate (136 B/term against ~2.2 ns of compute per term), so the
+// passes are equal, MSM_MAX_SLOTS of them.
 template <class C>
 int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scalars, size_t n, uint32_t scalar_mont,
-               uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
+               uint64_t* out_jac, ecg_abort_cb abort_cb, void* user, const MsmFill* fill) {
   using F = typename C::Fq;
   using X = XYZZ<F>;
   using HX = host::HPoint<HostF<C>>;
@@ -1711,11 +1716,18 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
     return ECG_OK;
   }
   const bool resident = bf.prepared;
-  const size_t bb = 2 * sizeof(F), sb = 32;
+  const size_t sb = 32;
+  // host bytes per base of the pass uploads: [x, y], the fill's layout, or none
+  const size_t bb = fill ? (fill->ark ? 2 * sizeof(F) + 8 : 2 * sizeof(F)) : (resident ? 0 : 2 * sizeof(F));
+  const void* hb = fill ? fill->h_bases : bases;
   // ---- pass sizes
   const size_t maxpass = msm_pass_terms<C>(ctx);
   std::vector<size_t> poff{0};
-  if (n >= ((size_t)1 << 22) && resident) {
+  if (fill && n >= ((size_t)1 << 22)) {
+    const size_t pass = std::min(maxpass, (n + MSM_MAX_SLOTS - 1) / MSM_MAX_SLOTS);
+    for (size_t o = pass; o < n; o += pass) poff.push_back(o);
+    poff.push_back(n);
+  } else if (n >= ((size_t)1 << 22) && resident && !fill) {
     // A/B: ECG_MSM_PASS_FIRST (1/x of n) and ECG_MSM_PASS_GROWTH
     static const uint32_t first_div = std::max(1u, env_u32("ECG_MSM_PASS_FIRST", 16));
     static const uint32_t growth = std::max(2u, env_u32("ECG_MSM_PASS_GROWTH", 3));
@@ -1743,13 +1755,14 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
   const uint32_t slots = (uint32_t)std::min<size_t>(np, MSM_MAX_SLOTS);
   // bytes per base of the resident buffer (all of its table rows)
   const size_t rstride = msm_base_record_bytes<C>() * (bf.tab_c ? msm_table_windows<C>(bf.tab_c) : 1u);
-  void *ib[2] = {nullptr, nullptr}, *is[2] = {nullptr, nullptr}, *sums;
-  if (!resident) ECG_TRY(ws_get(ctx, "msm_in_bases", pmax * bb, &ib[0]));
+  void *ib[2] = {nullptr, nullptr}, *is[2] = {nullptr, nullptr}, *sums, *fxy = nullptr;
+  if (bb) ECG_TRY(ws_get(ctx, "msm_in_bases", pmax * bb, &ib[0]));
   ECG_TRY(ws_get(ctx, "msm_in_scalars", pmax * sb, &is[0]));
   if (np > 1) {
-    if (!resident) ECG_TRY(ws_get(ctx, "msm_in_bases_b", pmax * bb, &ib[1]));
+    if (bb) ECG_TRY(ws_get(ctx, "msm_in_bases_b", pmax * bb, &ib[1]));
     ECG_TRY(ws_get(ctx, "msm_in_scalars_b", pmax * sb, &is[1]));
   }
+  if (fill && fill->ark) ECG_TRY(ws_get(ctx, "msm_fill_xy", pmax * 2 * sizeof(F), &fxy));
   ECG_TRY(ws_get(ctx, "msm_pass_sums", nbatch * nsums * sizeof(X), &sums));
   if (!ctx->copy_stream) ECG_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
   hipStream_t cs = ctx->stream, us = ctx->copy_stream;
@@ -1767,8 +1780,7 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
   auto upload = [&](size_t k) -> int {
     const size_t off = poff[k], m = poff[k + 1] - off;
     const int b = (int)(k & 1);
-    if (!resident)
-      ECG_HIP(hipMemcpyAsync(ib[b], (const uint8_t*)bases + off * bb, m * bb, hipMemcpyHostToDevice, us));
+    if (bb) ECG_HIP(hipMemcpyAsync(ib[b], (const uint8_t*)hb + off * bb, m * bb, hipMemcpyHostToDevice, us));
     ECG_HIP(hipMemcpyAsync(is[b], (const uint8_t*)h_scalars + off * sb, m * sb, hipMemcpyHostToDevice, us));
     ECG_HIP(hipEventRecord(up[b], us));
     return ECG_OK;
@@ -1788,6 +1800,14 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
     const void* bp = resident ? (const void*)((const uint8_t*)bases + poff[k] * rstride) : ib[b];
     rc = [&]() -> int {
       ECG_HIP(hipStreamWaitEvent(cs, up[b], 0));
+      if (fill) {  // this pass's records of the cache entry, from the uploaded host bases
+        const void* xy = ib[b];
+        if (fill->ark) {
+          ECG_TRY(bases_from_ark(ctx, fill->curve_id, ib[b], m, fxy, cs));
+          xy = fxy;
+        }
+        ECG_TRY(msm_records_t<C>(xy, m, const_cast<void*>(bp), cs));
+      }
       void* d_sums = nullptr;
       ECG_TRY(msm_core_t<C>(ctx, bp, is[b], g, pl, cs, &d_sums, resident, nullptr, CORE_ACC, MsmSlots{slot, slots}));
       ECG_HIP(hipEventRecord(done[b], cs));

@@ -22,7 +22,7 @@ struct MsmOps {
   // host scalars, pipelined with compute; bases on the host ([x, y]), or with
   // bf.prepared a device-resident prepared buffer
   int (*host)(ecg_ctx*, const void* bases, BaseForm bf, const void* h_scalars, size_t n, uint32_t scalar_mont,
-              uint64_t* out_jac, ecg_abort_cb, void* user);
+              uint64_t* out_jac, ecg_abort_cb, void* user, const MsmFill* fill);
   size_t (*record_bytes)();  // bytes per prepared base record (one table row)
   int (*plan_info)(size_t n, uint32_t window_bits, uint32_t* c, uint32_t* windows, int* sort_mode);
 };

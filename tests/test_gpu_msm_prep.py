@@ -167,6 +167,13 @@ def test_cached_ark_pipelined_2p22(gpu_programs, cname, cid):
     E_kat[[i - skip for i in ident]] = 0  # identity bases: their terms vanish
     kat = co.kat_scalar(cid, (a + skip * b) % r_int, b, E_kat, nthreads=16) % r_int
     assert (co.jac_to_affine(cid, first) == co.jac_to_affine(cid, co.gen_mul(cid, kat))).all()
+    # cold fill (skip 0, every base used): the cache entry is built pass by pass
+    # inside the pipelined MSM -- ark records and [x, y] records
+    for arr, ark_l in ((ark[skip:], True), (np.ascontiguousarray(xy[skip:]), False)):
+        k.clear_base_cache()
+        cold = k.multiexp_ex(arr, E, 0, ark_affine=ark_l, cache_bases=True)
+        hit = k.multiexp_ex(arr, E, 0, ark_affine=ark_l, cache_bases=True)
+        assert (cold == resident).all() and (hit == resident).all()
     k.clear_base_cache()
     d_xy.free()
     d_e.free()
