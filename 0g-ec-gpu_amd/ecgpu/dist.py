@@ -393,7 +393,9 @@ def comm_init_host(prog, rank: int, world: int, exchange: Callable[[int, bytes, 
                 return 1
             ctypes.memmove(recv, out, len(out))
             return 0
-        except Exception:  # noqa: BLE001 -- any transport failure is a failed exchange
+        except Exception as e:  # noqa: BLE001 -- any transport failure is a failed exchange
+            import sys
+            print(f"ecgpu.dist: host exchange on rank {rank} failed: {type(e).__name__}: {e}", file=sys.stderr)
             return 1
 
     c_cb = ecgpu.XCHG_CB(cb)
@@ -435,10 +437,14 @@ class LocalExchange:
 
 def hostgroup_exchange(group: "HostGroup", piece: int = 256 << 10) -> Callable[[int, bytes, int], bytes]:
     """comm_init_host callable over a HostGroup.  Its frames are capped at
-    1 MiB (hex-encoded), so payloads go in pieces of `piece` bytes, one
-    all-gather each -- meant for the status records and partial points, and
-    for rehearsal-size all-to-alls, not for bulk data."""
+    1 MiB and carry bytes hex-encoded, and rank 0's all-gather reply holds
+    every rank's piece, so payloads go in pieces of at most `piece` bytes and
+    at most (cap - slack) / (2 x world) -- one all-gather each.  Meant for the
+    status records and partial points, and for rehearsal-size all-to-alls, not
+    for bulk data."""
     import ecgpu
+
+    piece = max(1, min(piece, (HostGroup._MAX_FRAME - 4096) // (2 * max(group.world, 1))))
 
     def exchange(op: int, data: bytes, nbytes: int) -> bytes:
         parts = [group.allgather(data[o:o + piece]) for o in range(0, max(len(data), 1), piece)]

@@ -221,3 +221,31 @@ def test_hostgroup_exchange_allgather_alltoall_in_pieces():
         ag, a2a = out[r]
         assert ag == b"".join(bytes([q]) * nb for q in range(world))
         assert a2a == b"".join(bytes([16 * q + r]) * nb for q in range(world))
+
+
+def test_hostgroup_exchange_default_pieces_fit_the_frame_cap():
+    """The default piece size shrinks with the world so rank 0's all-gather
+    reply (every rank's piece, hex-encoded) stays under the frame cap: a
+    multi-MiB all-to-all at world 4 goes through."""
+    import ecgpu
+
+    port = _free_port()
+    world, nb = 4, 600 << 10
+    out = {}
+
+    def rank(r):
+        g = edist.HostGroup(r, world, "127.0.0.1", port, key=b"y" * 32, timeout=60)
+        try:
+            ex = edist.hostgroup_exchange(g)
+            send = b"".join(bytes([16 * r + q]) * nb for q in range(world))
+            out[r] = ex(ecgpu.XCHG_ALLTOALL, send, nb)
+        finally:
+            g.close()
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    for r in range(world):
+        assert out[r] == b"".join(bytes([16 * q + r]) * nb for q in range(world))
