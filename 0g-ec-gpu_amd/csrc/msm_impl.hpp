@@ -856,17 +856,20 @@ static uint32_t offset_bits(uint32_t S) {  // KB of msm_offset_bits_kernel
   return kb;
 }
 
-// Inputs per thread of msm_offset_bits_kernel: enough that one workgroup
-// covers a bit group (2^(KB-1) inputs: K = 2^(KB-9)), within [2, 32].  The
-// launch then has ~G (KB + 1) workgroups, under one per CU.  Measured at 2^20
-// (G = 16, S = 4096): K = 2 / 4 / 8 / 16 / 32 -> 0.67 / 0.54 / 0.45 / 0.38 /
-// 0.59 ms for the offset and A sums (profiles/r04/offset_bits_k_ab.txt); the
-// segment offsets and A tree of round 3 took 0.83 ms.  ECG_MSM_BITS_K pins K.
+// Inputs per thread of msm_offset_bits_kernel: enough that half a workgroup
+// covers a bit group (2^(KB-1) inputs: K = 2^(KB-8)) and the A sum needs no
+// second tree launch, within [2, 32].  The launch then has ~G (KB + 1)
+// workgroups, under one per CU.  Measured at 2^20 (G = 16, S = 4096, KB = 12):
+// K = 2 / 4 / 8 / 16 / 32 -> 0.67 / 0.54 / 0.45 / 0.38 / 0.59 ms for the
+// offset and A sums (profiles/r04/offset_bits_k_ab.txt); the segment offsets
+// and A tree of round 3 took 0.83 ms.  2^20 MSM 4.11 -> 4.05 ms with K = 16
+// over K = 8; 2^26 (KB = 13) K = 32 within noise of 16
+// (profiles/r04/tail_ls_k_ab.txt).  ECG_MSM_BITS_K pins K.
 static uint32_t offset_bits_k(uint32_t S) {
   const uint32_t pinned = env_u32("ECG_MSM_BITS_K", 0);
   if (pinned) return pinned;
   const uint32_t kb = offset_bits(S);
-  const uint32_t k = kb > 9 ? 1u << (kb - 9) : 2u;
+  const uint32_t k = kb > 8 ? 1u << (kb - 8) : 2u;
   return std::min(32u, std::max(2u, k));
 }
 
