@@ -1196,9 +1196,9 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   size_t tmp_bytes = 0;
   ECG_HIP(msm_sort(cfg, nullptr, tmp_bytes, (uint64_t*)e0, (uint64_t*)e1, sort_n, 0, sort_bits, s));
   ECG_TRY(ws_get(ctx, "msm_sort_tmp", tmp_bytes, &tmp));
-  if (msm_short_runs() && 2 * nseg_all < msm_short_max_recs()) {
+  if (msm_short_runs()) {  // the short pass runs at the first level below msm_short_max_recs records
     void* ks;
-    ECG_TRY(ws_get(ctx, "msm_rkeys_short", 2 * nseg_all * 4, &ks));
+    ECG_TRY(ws_get(ctx, "msm_rkeys_short", std::min(2 * nseg_all, msm_short_max_recs()) * 4, &ks));
   }
   if constexpr (!std::is_same<F, typename C::Fq>::value) {
     if (!prepared) {
@@ -1256,25 +1256,31 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   ECG_HIP(hipGetLastError());
   ECG_TRY(kt_end(ctx, "msm_accumulate", s));
 
-  // combine the segment-edge partials: the short runs in one launch, then
-  // what is left level by level
+  // combine the segment-edge partials level by level until fewer than
+  // msm_short_max_recs records are left, then the short runs in one launch
+  // and what is left level by level.  Large MSMs reach the short pass after
+  // one or two throughput-bound levels: the record list then holds exactly
+  // the buckets not yet stored (a level stores a bucket once all its records
+  // met), so the short pass completes them as it does at the first level.
+  // 2^26: levels 3-12 (0.68 ms, latency-bound from level 4 on) -> one short
+  // pass (profiles/r04/combine_short_late_ab.txt).
   size_t nrec = 2 * nseg_all;
   X* rin = (X*)rc;
   uint32_t* kin = (uint32_t*)rk;
   X* rout = (X*)rc2;
   uint32_t* kout = (uint32_t*)rk2;
   const uint32_t* lflag = nullptr;
-  if (msm_short_runs() && nrec < msm_short_max_recs()) {
-    void* ks;
-    ECG_TRY(ws_get(ctx, "msm_rkeys_short", nrec * 4, &ks));
-    hipLaunchKernelGGL(msm_combine_short_kernel<F>,
-                       dim3(blocks_for((nrec + MSM_SHORT_SEG - 1) / MSM_SHORT_SEG, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                       (const X*)rin, (const uint32_t*)kin, nrec, sentinel, (X*)bk, (uint32_t*)ks, long_runs);
-    ECG_HIP(hipGetLastError());
-    kin = (uint32_t*)ks;
-    lflag = long_runs;
-  }
   for (;;) {
+    if (!lflag && msm_short_runs() && nrec < msm_short_max_recs()) {
+      void* ks;
+      ECG_TRY(ws_get(ctx, "msm_rkeys_short", nrec * 4, &ks));
+      hipLaunchKernelGGL(msm_combine_short_kernel<F>,
+                         dim3(blocks_for((nrec + MSM_SHORT_SEG - 1) / MSM_SHORT_SEG, MSM_THREADS)), dim3(MSM_THREADS), 0,
+                         s, (const X*)rin, (const uint32_t*)kin, nrec, sentinel, (X*)bk, (uint32_t*)ks, long_runs);
+      ECG_HIP(hipGetLastError());
+      kin = (uint32_t*)ks;
+      lflag = long_runs;
+    }
     const bool fin = nrec <= comb_seg;
     const size_t nthr = (nrec + comb_seg - 1) / comb_seg;
     hipLaunchKernelGGL(msm_combine_kernel<F>, dim3(blocks_for(nthr, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
