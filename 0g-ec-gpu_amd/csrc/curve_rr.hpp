@@ -195,6 +195,151 @@ ECG_DEV XYZZ<FpR<Q>> rr_add_xyzz(const XYZZ<FpR<Q>>& p, const XYZZ<FpR<Q>>& q) {
 }
 
 // ---------------------------------------------------------------------------
+// Lane-pair forms for latency-bound chains.  A wave issues at most one VALU
+// instruction every ~2 quad-cycles when it is alone on its SIMD
+// (profiles/r04/mad_latency.txt: ~4 ns per v_mad_u64_u32 for one wave, with 1
+// to 8 independent chains alike), so a chain of point operations at under one
+// wave per SIMD runs at about half the issue rate whatever its ILP.  Fewer
+// instructions per wave per operation is what shortens it: two lanes (the
+// pair lane ^ M, M = 1 or 2) hold the same operands and each computes half of
+// every level's products, exchanging results through DPP quad permutes.  The
+// values are those of rr_dbl / rr_add_xyzz (same formulas, same bounds), only
+// distributed; both lanes return the whole result.  Both lanes of a pair must
+// run the call together (pair-uniform control flow).
+// ---------------------------------------------------------------------------
+template <int M>
+ECG_DEV uint32_t lane_swap_u32(uint32_t v) {
+  static_assert(M == 1 || M == 2, "pairs are lanes ^ 1 or lanes ^ 2 of a quad");
+  // quad_perm [1,0,3,2] (0xB1) or [2,3,0,1] (0x4E)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, M == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false);
+}
+template <int M, class Q>
+ECG_DEV FpR<Q> rr_lane_swap(const FpR<Q>& a) {
+  FpR<Q> r;
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) r.v[i] = lane_swap_u32<M>(a.v[i]);
+  return r;
+}
+template <class Q>
+ECG_DEV FpR<Q> rr_pick(bool c, const FpR<Q>& a, const FpR<Q>& b) {  // c ? a : b
+  FpR<Q> r;
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) r.v[i] = c ? a.v[i] : b.v[i];
+  return r;
+}
+template <int M>
+ECG_DEV bool pair_hi() {
+  return (threadIdx.x & M) != 0;
+}
+
+// 2 P (dbl-2008-s-1, as rr_dbl) on a lane pair.  Lane lo / hi:
+//   level 1: V = U^2          | X2 = X^2
+//   level 2: W = U V, ZZ3 = V ZZ | S = X V, M^2
+//   level 3: ZZZ3 = W ZZZ      | Y3 = M (S - X3) + Y (k p - W)
+// with three exchanges (V | X2, W | S, then the outputs).
+template <int M, class Q>
+ECG_DEV XYZZ<FpR<Q>> rr_dbl_x2(const XYZZ<FpR<Q>>& p) {
+  using F = FpR<Q>;
+  if (xyzz_is_zero_rr(p)) return p;
+  const bool h = pair_hi<M>();
+  const F U = rr_add(p.Y, p.Y);
+  const F L1 = rr_sqr(rr_pick(h, p.X, U));
+  const F O1 = rr_lane_swap<M>(L1);
+  const F V = rr_pick(h, O1, L1), X2 = rr_pick(h, L1, O1);
+  const F Mm = rr_add(rr_add(X2, X2), X2);
+  F a0, a1;
+  rr_mul2(rr_pick(h, p.X, U), V, rr_pick(h, Mm, V), rr_pick(h, Mm, p.ZZ), a0, a1);
+  const F O2 = rr_lane_swap<M>(a0);
+  const F W = rr_pick(h, O2, a0), S = rr_pick(h, a0, O2);
+  F X3, D;  // meaningful on the hi lane (a1 = M^2 there)
+  if constexpr (rr_tight<Q>()) {
+    X3 = rr_reduce_q(rr_sub2<16>(a1, S, S));
+    D = rr_sub<4>(S, X3);
+  } else {
+    X3 = rr_sub2<16>(a1, S, S);
+    D = rr_sub<64>(S, X3);
+  }
+  const F z = F::zero();
+  const F r = rr_mul_sum2(rr_pick(h, Mm, W), rr_pick(h, D, p.ZZZ), rr_pick(h, p.Y, z), rr_pick(h, rr_neg<4>(W), z));
+  const F f = rr_lane_swap<M>(r);                   // lo <- Y3, hi <- ZZZ3
+  const F g = rr_lane_swap<M>(rr_pick(h, X3, a1));  // lo <- X3, hi <- ZZ3
+  XYZZ<F> o;
+  o.X = rr_pick(h, X3, g);
+  o.Y = rr_pick(h, r, f);
+  o.ZZ = rr_pick(h, g, a1);
+  o.ZZZ = rr_pick(h, f, r);
+  return o;
+}
+
+// P + Q (add-2008-s, as rr_add_xyzz) on a lane pair.  Lane lo / hi:
+//   level 1: U1 = X1 ZZ2, S1 = Y1 ZZZ2   | U2 = X2 ZZ1, S2 = Y2 ZZZ1
+//   level 2: PP = P^2, RR = R^2          | ZZ12, ZZZ12
+//   level 3: PPP = P PP, Q = U1 PP       | ZZ3 = ZZ12 PP
+//   level 4: Y3 = R (Q - X3) + S1 (k p - PPP) | ZZZ3 = ZZZ12 PPP
+template <int M, class Q>
+ECG_DEV XYZZ<FpR<Q>> rr_add_x2(const XYZZ<FpR<Q>>& p, const XYZZ<FpR<Q>>& q) {
+  using F = FpR<Q>;
+  const bool pz = xyzz_is_zero_rr(p), qz = xyzz_is_zero_rr(q);
+  XYZZ<F> o;
+  if (pz || qz) {
+    o = q;
+    rr_sel(o, qz, p);
+    return o;
+  }
+  const bool h = pair_hi<M>();
+  F a0, a1;
+  rr_mul2(rr_pick(h, q.X, p.X), rr_pick(h, p.ZZ, q.ZZ), rr_pick(h, q.Y, p.Y), rr_pick(h, p.ZZZ, q.ZZZ), a0, a1);
+  const F e0 = rr_lane_swap<M>(a0), e1 = rr_lane_swap<M>(a1);
+  const F U1 = rr_pick(h, e0, a0), U2 = rr_pick(h, a0, e0);
+  const F S1 = rr_pick(h, e1, a1), S2 = rr_pick(h, a1, e1);
+  const F P = rr_sub<4>(U2, U1);
+  const F R = rr_sub<4>(S2, S1);
+  F b0, b1;  // lo: PP, RR | hi: ZZ12, ZZZ12
+  rr_mul2(rr_pick(h, p.ZZ, P), rr_pick(h, q.ZZ, P), rr_pick(h, p.ZZZ, R), rr_pick(h, q.ZZZ, R), b0, b1);
+  const F e2 = rr_lane_swap<M>(b0);
+  const F PP = rr_pick(h, e2, b0), ZZ12 = rr_pick(h, b0, e2);
+  F c0, c1;  // lo: PPP, Q | hi: ZZ3 (twice)
+  rr_mul2(rr_pick(h, ZZ12, P), PP, rr_pick(h, ZZ12, U1), PP, c0, c1);
+  const F e3 = rr_lane_swap<M>(c0);
+  const F PPP = rr_pick(h, e3, c0), ZZ3 = rr_pick(h, c0, e3);
+  F X3, D;  // meaningful on the lo lane (b1 = RR, c1 = Q there)
+  if constexpr (rr_tight<Q>()) {
+    X3 = rr_reduce_q(rr_sub3<16>(b1, PPP, c1, c1));
+    D = rr_sub<4>(c1, X3);
+  } else {
+    X3 = rr_sub3<16>(b1, PPP, c1, c1);
+    D = rr_sub<64>(c1, X3);
+  }
+  const F z = F::zero();
+  const F r = rr_mul_sum2(rr_pick(h, b1, R), rr_pick(h, PPP, D), rr_pick(h, z, S1), rr_pick(h, z, rr_neg<4>(PPP)));
+  const F f = rr_lane_swap<M>(r);   // lo <- ZZZ3, hi <- Y3
+  const F g = rr_lane_swap<M>(X3);  // hi <- X3
+  o.X = rr_pick(h, g, X3);
+  o.Y = rr_pick(h, f, r);
+  o.ZZ = ZZ3;
+  o.ZZZ = rr_pick(h, r, f);
+  if (rr_maybe_zero_prod(PP)) {  // rare, pair-uniform (both lanes hold PP): P = Q or P = -Q
+    const F RRv = rr_pick(h, rr_lane_swap<M>(b1), b1);
+    const bool inf = rr_is_zero_prod(PP);
+    const bool dbl = inf && rr_is_zero_prod(RRv);
+    XYZZ<F> d = xyzz_zero<F>();
+    if (dbl) d = rr_dbl_x2<M>(p);
+    rr_sel(o, inf, d);
+  }
+  return o;
+}
+
+// lane-pair forms exist for the reduced-radix G1 points
+template <class PF>
+struct PairOps {
+  static constexpr bool ok = false;
+};
+template <class Q>
+struct PairOps<FpR<Q>> {
+  static constexpr bool ok = true;
+};
+
+// ---------------------------------------------------------------------------
 // point-arithmetic policy used by the MSM kernels (msm_impl.hpp): one name per
 // operation, overloaded on the coordinate field -- the 32-bit-limb lazy
 // formulas of curve.hpp (G2 over Fq2, A/B) or the reduced-radix ones above.
@@ -224,6 +369,23 @@ ECG_DEV XYZZ<F> pa_dbl(const XYZZ<F>& p) {
 template <class Q>
 ECG_DEV XYZZ<FpR<Q>> pa_dbl(const XYZZ<FpR<Q>>& p) {
   return rr_dbl(p);
+}
+
+// Point operations of latency-bound chains: one lane per operation (PM = 0),
+// or a lane pair (lanes ^ PM) sharing each operation's products
+template <int PM, class PF>
+ECG_DEV XYZZ<PF> pp_dbl(const XYZZ<PF>& p) {
+  if constexpr (PM != 0)
+    return rr_dbl_x2<PM>(p);
+  else
+    return pa_dbl(p);
+}
+template <int PM, class PF>
+ECG_DEV XYZZ<PF> pp_add(const XYZZ<PF>& p, const XYZZ<PF>& q) {
+  if constexpr (PM != 0)
+    return rr_add_x2<PM>(p, q);
+  else
+    return pa_add(p, q);
 }
 
 template <class F>

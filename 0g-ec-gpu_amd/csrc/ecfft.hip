@@ -243,20 +243,20 @@ ECG_DEV T sel_words(bool c, const T& a, const T& b) {  // c ? a : b
   return r;
 }
 
-template <class T>
-ECG_DEV T shfl_xor1(const T& v) {  // the partner lane's value (lanes 2u <-> 2u + 1)
+template <int X = 1, class T>
+ECG_DEV T shfl_xor1(const T& v) {  // the partner lane's value (lanes u <-> u ^ X)
   constexpr int NW = (int)(sizeof(T) / 4);
   uint32_t w[NW];
   __builtin_memcpy(w, &v, sizeof(T));
 #pragma unroll
-  for (int i = 0; i < NW; i++) w[i] = (uint32_t)__shfl_xor((int)w[i], 1);
+  for (int i = 0; i < NW; i++) w[i] = (uint32_t)__shfl_xor((int)w[i], X);
   T r;
   __builtin_memcpy(&r, w, sizeof(T));
   return r;
 }
 
 // k P, k little-endian in W words (signed 4-bit windows, see above)
-template <int W, class PF>
+template <int W, int PM = 0, class PF>
 ECG_DEV XYZZ<PF> win_mul(const XYZZ<PF>& P, const uint32_t* k, XYZZ<PF>* __restrict__ tab) {
   uint32_t K[W + 1];
   uint64_t c = 0;
@@ -269,17 +269,17 @@ ECG_DEV XYZZ<PF> win_mul(const XYZZ<PF>& P, const uint32_t* k, XYZZ<PF>* __restr
   K[W] = (uint32_t)c + 8u;  // digit 8W in {0, 1}
   // table m P, m = 1..8: four levels (2P; 3P, 4P; 5P, 6P, 8P; 7P)
   store_xyzz(&tab[0], P);
-  const XYZZ<PF> P2 = pa_dbl(P);
+  const XYZZ<PF> P2 = pp_dbl<PM>(P);
   store_xyzz(&tab[1], P2);
-  const XYZZ<PF> P3 = pa_add(P2, P);
+  const XYZZ<PF> P3 = pp_add<PM>(P2, P);
   store_xyzz(&tab[2], P3);
-  const XYZZ<PF> P4 = pa_dbl(P2);
+  const XYZZ<PF> P4 = pp_dbl<PM>(P2);
   store_xyzz(&tab[3], P4);
-  store_xyzz(&tab[4], pa_add(P4, P));
-  const XYZZ<PF> P6 = pa_dbl(P3);
+  store_xyzz(&tab[4], pp_add<PM>(P4, P));
+  const XYZZ<PF> P6 = pp_dbl<PM>(P3);
   store_xyzz(&tab[5], P6);
-  store_xyzz(&tab[6], pa_add(P6, P));
-  store_xyzz(&tab[7], pa_dbl(P4));
+  store_xyzz(&tab[6], pp_add<PM>(P6, P));
+  store_xyzz(&tab[7], pp_dbl<PM>(P4));
   XYZZ<PF> acc = xyzz_zero<PF>();
 #pragma unroll 1
   for (int i = 8 * W; i >= 0; i--) {
@@ -289,24 +289,29 @@ ECG_DEV XYZZ<PF> win_mul(const XYZZ<PF>& P, const uint32_t* k, XYZZ<PF>* __restr
     const int d = (int)((word >> ((i & 7) * 4)) & 15u) - 8;
     const XYZZ<PF> T = load_xyzz(&tab[d < 0 ? -d - 1 : d > 0 ? d - 1 : 0]);  // issued before the doublings
 #pragma unroll 1
-    for (int b = 0; b < 4; b++) acc = pa_dbl(acc);
-    if (d != 0) acc = pa_add(acc, neg_if(T, d < 0));
+    for (int b = 0; b < 4; b++) acc = pp_dbl<PM>(acc);
+    if (d != 0) acc = pp_add<PM>(acc, neg_if(T, d < 0));
   }
   return acc;
 }
 
 // Stage s (as ecfft_stage_kernel) with windowed products; GLV curves: lanes
-// 2u, 2u + 1 share butterfly u (half 0: k1 P, half 1: k2 phi(P)).
-template <class C, class PF>
+// 2u, 2u + 1 share butterfly u (half 0: k1 P, half 1: k2 phi(P)).  With PM = 1
+// every lane of that layout becomes a lane pair (lanes 2v, 2v + 1) sharing
+// each point operation's products (pp_dbl / pp_add): 4 lanes per butterfly on
+// GLV curves, 2 otherwise, and the GLV partner is lane ^ 2.
+template <class C, class PF, int PM>
 __global__ void __launch_bounds__(ECFFT_THREADS)
     ecfft_stage_win_kernel(XYZZ<PF>* __restrict__ a, const uint4* __restrict__ tw, uint32_t log_n, uint32_t s,
                            uint32_t batch, XYZZ<PF>* __restrict__ tabs) {
   constexpr bool glv = has_glv<C>();
+  constexpr uint32_t PB = PM != 0 ? 1u : 0u;  // log2 lanes per point operation
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t lanes_log = glv ? log_n : log_n - 1;  // lanes per transform (2 per butterfly on GLV curves)
-  if (g >= (batch << lanes_log)) return;               // both lanes of a pair leave together
+  const uint32_t lanes_log = (glv ? log_n : log_n - 1) + PB;  // lanes per transform
+  if (g >= (batch << lanes_log)) return;               // the lanes of a butterfly leave together
   a += (size_t)(g >> lanes_log) << log_n;              // transform g >> lanes_log of the batch
-  const uint32_t gl = g & ((1u << lanes_log) - 1);
+  const uint32_t gl = (g & ((1u << lanes_log) - 1)) >> PB;
+  const bool lead = PM == 0 || (g & 1u) == 0;          // the lane of a pair that stores
   const uint32_t t = glv ? gl >> 1 : gl;
   const uint32_t half = glv ? (gl & 1) : 0u;
   const uint32_t h = 1u << s;
@@ -324,20 +329,33 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
       from_u64_words(beta, C::Gen::BETA);
       XYZZ<PF> Bh = B;
       Bh.X = sel_words(half != 0, pa_mul_const(B.X, beta), B.X);  // phi(x, y) = (beta x, y)
-      const XYZZ<PF> Rh = win_mul<4>(Bh, k, tabs + (size_t)ECFFT_TAB * g);
-      R = pa_add(Rh, shfl_xor1(Rh));
+      const XYZZ<PF> Rh = win_mul<4, PM>(Bh, k, tabs + (size_t)ECFFT_TAB * g);
+      R = pp_add<PM>(Rh, shfl_xor1<1 << PB>(Rh));
     } else {
       const uint4 lo = tw[2 * e], hi = tw[2 * e + 1];
       const uint32_t k[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      R = win_mul<8>(B, k, tabs + (size_t)ECFFT_TAB * g);
+      R = win_mul<8, PM>(B, k, tabs + (size_t)ECFFT_TAB * g);
     }
   }
-  if constexpr (glv) {  // lane 0 writes A + wB, lane 1 A - wB
-    store_xyzz(&a[half ? i1 : i0], pa_add(A, neg_if(R, half != 0)));
+  if constexpr (glv) {  // half 0 writes A + wB, half 1 A - wB
+    const XYZZ<PF> o = pp_add<PM>(A, neg_if(R, half != 0));
+    if (lead) store_xyzz(&a[half ? i1 : i0], o);
+  } else if constexpr (PM != 0) {  // the pair's lanes store one output each
+    const XYZZ<PF> o0 = pp_add<PM>(A, R);
+    const XYZZ<PF> o1 = pp_add<PM>(A, pa_neg(R));
+    store_xyzz(&a[lead ? i0 : i1], lead ? o0 : o1);
   } else {
     store_xyzz(&a[i0], pa_add(A, R));
     store_xyzz(&a[i1], pa_add(A, pa_neg(R)));
   }
+}
+
+static bool ecfft_pairs_enabled() {  // A/B switch: ECG_ECFFT_PAIRS=0 keeps one lane per point operation
+  static const bool v = [] {
+    const char* e = getenv("ECG_ECFFT_PAIRS");
+    return !(e && e[0] == '0');
+  }();
+  return v;
 }
 
 static bool ecfft_win_enabled() {  // A/B switch: ECG_ECFFT_WIN=0 keeps the bit ladders (ecfft_stage_kernel)
@@ -390,7 +408,14 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
   void *a, *tw, *gt = nullptr;
   ECG_TRY(ws_get(ctx, "ecfft_pts", nb * sizeof(XYZZ<PF>), &a));
   ECG_TRY(ws_get(ctx, "ecfft_tw", (size_t)(n / 2 + 1) * 32, &tw));
-  const size_t lanes = has_glv<C>() && win ? nb : (size_t)batch * (n / 2) + 1;  // stage lanes (2 per butterfly on GLV curves)
+  // lane pairs while the paired stage still leaves each SIMD at most one
+  // wave (2^15 lanes before pairing): 2^10-2^14 G1 stages 33 % faster; at
+  // 2^16 (one wave per SIMD unpaired) pairs are 26 % slower
+  // (profiles/r04/lane_pairs_ab.txt)
+  const size_t lanes1 = has_glv<C>() && win ? nb : (size_t)batch * (n / 2);
+  const bool pairs = win && PairOps<PF>::ok && ecfft_pairs_enabled() && lanes1 <= ((size_t)1 << 15);
+  // stage lanes: 2 per butterfly on GLV curves, doubled by lane pairs
+  const size_t lanes = (lanes1 << (pairs ? 1 : 0)) + 1;
   if (win)
     ECG_TRY(ws_get(ctx, "ecfft_tab", lanes * ECFFT_TAB * sizeof(XYZZ<PF>), &gt));
   else if (has_glv<C>())
@@ -413,10 +438,17 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
     }
     ECG_TRY(kt_begin(ctx, "ecfft_stage", s));
     if constexpr (!std::is_same<PF, F>::value) {
-      if (win)
-        hipLaunchKernelGGL((ecfft_stage_win_kernel<C, PF>), dim3(ecfft_blocks(has_glv<C>() ? nb : nb / 2)),
+      const size_t stage_lanes = has_glv<C>() ? nb : nb / 2;
+      if (win && pairs) {
+        if constexpr (PairOps<PF>::ok)
+          hipLaunchKernelGGL((ecfft_stage_win_kernel<C, PF, 1>), dim3(ecfft_blocks(2 * stage_lanes)),
+                             dim3(ECFFT_THREADS), 0, s, (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, batch,
+                             (XYZZ<PF>*)gt);
+      } else if (win) {
+        hipLaunchKernelGGL((ecfft_stage_win_kernel<C, PF, 0>), dim3(ecfft_blocks(stage_lanes)),
                            dim3(ECFFT_THREADS), 0, s, (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, batch,
                            (XYZZ<PF>*)gt);
+      }
     }
     if (!win)
       hipLaunchKernelGGL((ecfft_stage_kernel<C, PF>), dim3(ecfft_blocks(n / 2)), dim3(ECFFT_THREADS), 0, s,

@@ -201,6 +201,7 @@ static void plan_reduction(MsmPlan& pl, uint32_t waves = 2) {
 // below) per task (bucket accumulation vs reduction vs window-fold adds; a
 // reduction step is ~2 full adds, ~1.4x a mixed add).  nbits = scalar MODULUS_BIT_SIZE.  forced_c != 0 pins c.
 static MsmPlan make_plan(size_t n, uint32_t nbits, uint32_t forced_c = 0) {
+  if (!forced_c) forced_c = env_u32("ECG_MSM_C", 0);  // A/B: pin the single-MSM window
   double best = 1e300;
   MsmPlan pl{};
   for (uint32_t c = 1; c <= 22; c++) {
@@ -698,14 +699,17 @@ struct LdsPoint {  // XYZZ<F> words of lane t at w[i * MSM_THREADS + t]
 // Several bucket arrays (slots, `slot_stride` buckets apart) hold the buckets
 // of the passes of one MSM (msm_host_t): bucket j is their sum, added into the
 // running sum slot by slot -- one reduction for every pass.
-template <class F>
+// PM = 1: a lane pair per segment (pp_add), for launches under one wave per
+// SIMD (msm_tail_pairs).
+template <class F, int PM>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
     msm_reduce_kernel(const XYZZ<F>* __restrict__ buckets, MsmPlan pl, XYZZ<F>* __restrict__ partial,
                       XYZZ<F>* __restrict__ runs, uint32_t slots, size_t slot_stride) {
   __shared__ uint32_t lds[LdsPoint<F>::NW * MSM_THREADS];
   const LdsPoint<F> acc_l{lds};
-  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= pl.G * pl.S) return;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t id = PM != 0 ? g >> 1 : g;
+  if (id >= pl.G * pl.S) return;  // both lanes of a pair leave together
   const uint32_t w = id / pl.S, sgm = id % pl.S;
   const XYZZ<F>* bk = buckets + (size_t)w * pl.B + (size_t)sgm * pl.LS;
   const uint32_t len = min(pl.LS, pl.B - sgm * pl.LS);  // the last segment may be shorter
@@ -713,12 +717,14 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
   acc_l.put(xyzz_zero<F>());
   for (int j = (int)len - 1; j >= 0; j--) {
 #pragma unroll 1
-    for (uint32_t q = 0; q < slots; q++) run = pa_add(run, load_xyzz(&bk[q * slot_stride + j]));
-    acc_l.put(pa_add(acc_l.get(), run));
+    for (uint32_t q = 0; q < slots; q++) run = pp_add<PM>(run, load_xyzz(&bk[q * slot_stride + j]));
+    acc_l.put(pp_add<PM>(acc_l.get(), run));
   }
   // acc = sum_j (j+1) S_j ; run = sum_j S_j
-  store_xyzz(&partial[id], acc_l.get());
-  store_xyzz(&runs[id], run);
+  if (PM == 0 || (g & 1u) == 0) {
+    store_xyzz(&partial[id], acc_l.get());
+    store_xyzz(&runs[id], run);
+  }
 }
 
 // partial[id] += (sgm LS) run_sgm  (segment offset of the bucket weights)
@@ -811,43 +817,65 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
 //     K serially per thread, then log2(256) LDS levels.  Every add here waits
 //     for the previous one (~15 us for a full add at this occupancy), so the
 //     launch is sized by K (offset_bits_k) to ~one workgroup per CU.
-template <class F>
+//     PM = 1: lane pairs (pp_add), MSM_THREADS / 2 per workgroup; the lead
+//     lane of a pair writes its LDS slot.
+template <class F, int PM>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
     msm_offset_bits_kernel(const XYZZ<F>* __restrict__ partial, const XYZZ<F>* __restrict__ runs, uint32_t S,
                            uint32_t KB, uint32_t K, uint32_t wgs, XYZZ<F>* __restrict__ out) {
   extern __shared__ uint32_t lds_pts[];
   const LdsPoints<F> pts{lds_pts};
-  const uint32_t g = blockIdx.x / wgs, b = blockIdx.x % wgs, t = threadIdx.x;
+  constexpr uint32_t PB = PM != 0 ? 1u : 0u;
+  constexpr uint32_t NT = MSM_THREADS >> PB;  // operation lanes (pairs) per workgroup
+  const uint32_t g = blockIdx.x / wgs, b = blockIdx.x % wgs, t = threadIdx.x >> PB;
+  const bool lead = PM == 0 || (threadIdx.x & 1u) == 0;
   const uint32_t w = g / (KB + 1), k = g % (KB + 1);
   const bool a_sum = k == KB;
   const XYZZ<F>* src = (a_sum ? partial : runs) + (size_t)w * S;
   const uint32_t cnt = a_sum ? S : (1u << (KB - 1));
-  const uint32_t span = MSM_THREADS * K;
+  const uint32_t span = NT * K;
   if (b * span >= cnt) {  // this group has fewer inputs than the widest one: the identity
-    if (t == 0) store_xyzz(&out[blockIdx.x], xyzz_zero<F>());
+    if (threadIdx.x == 0) store_xyzz(&out[blockIdx.x], xyzz_zero<F>());
     return;
   }
-  const uint32_t j0 = (b * MSM_THREADS + t) * K;
+  const uint32_t j0 = (b * NT + t) * K;
   XYZZ<F> acc = xyzz_zero<F>();
 #pragma unroll 1
   for (uint32_t q = 0; q < K; q++) {
     const uint32_t i = j0 + q;
     if (i >= cnt) break;
     const uint32_t sg = a_sum ? i : (((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1)));
-    if (sg < S) acc = pa_add(acc, load_xyzz(&src[sg]));
+    if (sg < S) acc = pp_add<PM>(acc, load_xyzz(&src[sg]));
   }
-  pts.put(t, acc);
+  if (lead) pts.put(t, acc);
   __syncthreads();
   const uint32_t left = cnt - b * span;
-  const uint32_t active = left >= span ? MSM_THREADS : (left + K - 1) / K;
+  const uint32_t active = left >= span ? NT : (left + K - 1) / K;
   uint32_t top = 1;
   while (top < active) top <<= 1;
 #pragma unroll 1
   for (uint32_t stride = top / 2; stride > 0; stride >>= 1) {
-    if (t < stride) pts.put(t, pa_add(pts.get(t), pts.get(t + stride)));
+    // a pair reads slots t and t + stride before its lead lane writes slot t
+    // (LDS operations of one wave complete in order); no other pair touches
+    // slot t at this level
+    if (t < stride) {
+      const XYZZ<F> v = pp_add<PM>(pts.get(t), pts.get(t + stride));
+      if (lead) pts.put(t, v);
+    }
     __syncthreads();
   }
-  if (t == 0) store_xyzz(&out[blockIdx.x], pts.get(0));
+  if (threadIdx.x == 0) store_xyzz(&out[blockIdx.x], pts.get(0));
+}
+
+// Lane pairs in the reduction tail (A/B: ECG_MSM_TAIL_PAIRS, a bit mask:
+// 1 = offset-bit sums, 2 = running sums of launches at or under half a wave
+// per SIMD).  A pair pays off only while the paired launch still leaves each
+// SIMD at most one wave: from one wave to two, the extra exchange and select
+// instructions cost what the shorter chains save (EC-FFT 2^16: 26.6 -> 33.6
+// ms, profiles/r04/lane_pairs_ab.txt).
+static uint32_t msm_tail_pairs() {
+  static const uint32_t v = env_u32("ECG_MSM_TAIL_PAIRS", 1);
+  return v;
 }
 
 static uint32_t offset_bits(uint32_t S) {  // KB of msm_offset_bits_kernel
@@ -944,22 +972,28 @@ __global__ void msm_sums_to_std_kernel(const XYZZ<F>* __restrict__ in, uint32_t 
 }
 
 // Batched form: the per-task Horner over its W window sums in the pipeline's
-// reduced-radix point form, before the conversion (one thread per task).  The
-// fold is a latency-bound chain of c (W - 1) doublings -- 1024 tasks are 16
-// waves on 1024 SIMDs -- and the reduced-radix formulas issue their paired
-// products as independent chains where the 32-bit-limb ones wait on carries.
-template <class F>
+// reduced-radix point form, before the conversion.  The fold is a
+// latency-bound chain of c (W - 1) doublings -- 1024 tasks are 16 waves on
+// 1024 SIMDs, each wave alone on its SIMD -- so on G1 a lane pair takes each
+// task (PM = 1: pp_dbl / pp_add share every operation's products) and a wave
+// issues about half the instructions per doubling.
+template <class F, int PM>
 __global__ void __launch_bounds__(64)
     msm_fold_rr_kernel(const XYZZ<F>* __restrict__ sums, uint32_t nw, uint32_t c, uint32_t tasks,
                        XYZZ<F>* __restrict__ out) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= tasks) return;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = PM != 0 ? g >> 1 : g;
+  if (t >= tasks) return;  // both lanes of a pair leave together
   XYZZ<F> acc = load_xyzz(&sums[(size_t)t * nw + nw - 1]);
   for (int w = (int)nw - 2; w >= 0; w--) {
-    for (uint32_t k = 0; k < c; k++) acc = pa_dbl(acc);
-    acc = pa_add(acc, load_xyzz(&sums[(size_t)t * nw + w]));
+    for (uint32_t k = 0; k < c; k++) acc = pp_dbl<PM>(acc);
+    acc = pp_add<PM>(acc, load_xyzz(&sums[(size_t)t * nw + w]));
   }
-  store_xyzz(&out[t], acc);
+  if (PM == 0 || (g & 1u) == 0) store_xyzz(&out[t], acc);
+}
+static bool msm_fold_pairs_enabled() {  // A/B switch: ECG_MSM_FOLD_PAIRS=0 keeps one lane per task
+  static const bool v = env_u32("ECG_MSM_FOLD_PAIRS", 1) != 0;
+  return v;
 }
 
 static bool msm_rr_enabled() {  // A/B switch: ECG_MSM_RR=0 runs the 32-bit-limb pipeline
@@ -1297,8 +1331,19 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
 
   void* runs;
   ECG_TRY(ws_get(ctx, "msm_runs", (size_t)pl.G * pl.S * sizeof(X), &runs));
-  hipLaunchKernelGGL(msm_reduce_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
-                     dim3(MSM_THREADS), 0, s, (const X*)bk_all, pl, (X*)pa, (X*)runs, nslots, (size_t)nb);
+  // lane pairs where the launch leaves a SIMD one wave or less (msm_tail_pairs)
+  const bool tail_pairs = PairOps<F>::ok && (msm_tail_pairs() & 1u);
+  bool red_paired = false;
+  if constexpr (PairOps<F>::ok) {
+    if ((msm_tail_pairs() & 2u) && (size_t)pl.G * pl.S <= MSM_RED_THREADS / 4) {
+      hipLaunchKernelGGL((msm_reduce_kernel<F, 1>), dim3(blocks_for(2 * (size_t)pl.G * pl.S, MSM_THREADS)),
+                         dim3(MSM_THREADS), 0, s, (const X*)bk_all, pl, (X*)pa, (X*)runs, nslots, (size_t)nb);
+      red_paired = true;
+    }
+  }
+  if (!red_paired)
+    hipLaunchKernelGGL((msm_reduce_kernel<F, 0>), dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
+                       dim3(MSM_THREADS), 0, s, (const X*)bk_all, pl, (X*)pa, (X*)runs, nslots, (size_t)nb);
   ECG_HIP(hipGetLastError());
   uint32_t cnt = pl.S;
   uint32_t groups = pl.G;
@@ -1308,18 +1353,28 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   if (tree_lds > 64 * 1024) {  // G2 points (96 KiB per workgroup) need the opt-in
     ECG_HIP(hipFuncSetAttribute((const void*)msm_tree_sum_kernel<F>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)tree_lds));
-    ECG_HIP(hipFuncSetAttribute((const void*)msm_offset_bits_kernel<F>,
+    ECG_HIP(hipFuncSetAttribute((const void*)msm_offset_bits_kernel<F, 0>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)tree_lds));
   }
   if (bits) {
     const uint32_t kb = offset_bits(pl.S);
     const uint32_t K = offset_bits_k(pl.S);
-    const uint32_t wgs = (pl.S + MSM_THREADS * K - 1) / (MSM_THREADS * K);
+    const uint32_t nt = tail_pairs ? MSM_THREADS / 2 : MSM_THREADS;  // operation lanes per workgroup
+    const uint32_t wgs = (pl.S + nt * K - 1) / (nt * K);
     groups = pl.G * (kb + 1);
     void* pbits;
     ECG_TRY(ws_get(ctx, "msm_pbits", (size_t)groups * wgs * sizeof(X), &pbits));
-    hipLaunchKernelGGL(msm_offset_bits_kernel<F>, dim3(groups * wgs), dim3(MSM_THREADS), tree_lds, s, (const X*)pa,
-                       (const X*)runs, pl.S, kb, K, wgs, (X*)pbits);
+    bool bits_paired = false;
+    if constexpr (PairOps<F>::ok) {
+      if (tail_pairs) {
+        hipLaunchKernelGGL((msm_offset_bits_kernel<F, 1>), dim3(groups * wgs), dim3(MSM_THREADS), tree_lds, s,
+                           (const X*)pa, (const X*)runs, pl.S, kb, K, wgs, (X*)pbits);
+        bits_paired = true;
+      }
+    }
+    if (!bits_paired)
+      hipLaunchKernelGGL((msm_offset_bits_kernel<F, 0>), dim3(groups * wgs), dim3(MSM_THREADS), tree_lds, s,
+                         (const X*)pa, (const X*)runs, pl.S, kb, K, wgs, (X*)pbits);
     ECG_HIP(hipGetLastError());
     in = (X*)pbits;
     cnt = wgs;
@@ -1355,8 +1410,17 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     uint32_t npts = pl.G;
     if (folded && pl.fold_windows() > 1 && ECG_MSM_FOLD_RR_ON) {  // batched: Horner per task first
       const uint32_t tasks = pl.G / pl.W;
-      hipLaunchKernelGGL(msm_fold_rr_kernel<F>, dim3(blocks_for(tasks, 64)), dim3(64), 0, s, (const X*)in, pl.W,
-                         pl.c, tasks, out);
+      bool paired = false;
+      if constexpr (PairOps<F>::ok) {
+        if (msm_fold_pairs_enabled()) {
+          hipLaunchKernelGGL((msm_fold_rr_kernel<F, 1>), dim3(blocks_for(2 * (size_t)tasks, 64)), dim3(64), 0, s,
+                             (const X*)in, pl.W, pl.c, tasks, out);
+          paired = true;
+        }
+      }
+      if (!paired)
+        hipLaunchKernelGGL((msm_fold_rr_kernel<F, 0>), dim3(blocks_for(tasks, 64)), dim3(64), 0, s, (const X*)in,
+                           pl.W, pl.c, tasks, out);
       ECG_HIP(hipGetLastError());
       in = out;
       npts = tasks;

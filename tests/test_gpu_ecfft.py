@@ -119,6 +119,31 @@ def test_gpu_ec_fft_many_and_unnormalised_inputs(kernels, cname, cid):
         assert same_points(cid, g, w)
 
 
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_gpu_ec_fft_equal_and_opposite_points(kernels, cname, cid):
+    """Inputs whose butterflies add a point to itself and to its negative: all
+    P_j equal (stage 0 computes P + P and P - P), and P_j = (-1)^j P.  These
+    take the doubling and identity branches of the full add (on G1 the lane-pair
+    form, curve_rr.hpp rr_add_x2), against serial_ec_fft."""
+    cv = po.CURVES[cname]
+    lq = cv.fq.limbs64
+    for log_d in (1, 4, 6):
+        n = 1 << log_d
+        P = co.gen_mul(cid, 987654321 + cid)
+        negP = co.gen_mul(cid, (cv.fr.modulus - 987654321 - cid) % cv.fr.modulus)
+        for pattern in ("equal", "alternating"):
+            if pattern == "equal":
+                pts = np.tile(P, (n, 1))
+            else:
+                pts = np.stack([P if j % 2 == 0 else negP for j in range(n)])
+            pts = np.ascontiguousarray(pts.reshape(n, 3 * lq))
+            om = omega_m(cv, n)
+            want = co.serial_ec_fft(cid, pts, om, log_d, nthreads=16)
+            got = pts.copy()
+            kernels[cname].radix_ec_fft(got, om, log_d)
+            assert same_points(cid, got, want), (log_d, pattern)
+
+
 def test_ag_cuda_ec_radix_ec_fft(gpu_programs):
     """ag-cuda-ec/src/ec_fft.rs:97-131: degrees 4..8, omegas[i] = omega^(2^i)."""
     prog = gpu_programs[0][0]

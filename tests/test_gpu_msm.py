@@ -364,6 +364,31 @@ def test_msm_skewed_scalars_2p22(gpu_programs, pattern):
 
 
 @pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_late_short_pass_2p23(gpu_programs, cname, cid):
+    """2^23 terms leave 2^21 segment-edge records: one combine level runs
+    first, and the short-run pass takes over at the next level (2^19 records).
+    Groups of 2000-12000 equal scalars make runs of about 4-24 level-1 records,
+    so the short pass meets runs on both sides of its 16-record limit, and
+    the long ones go on through the levels.  Checked by the KAT."""
+    cv = po.CURVES[cname]
+    prog = gpu_programs[0][0]
+    n = 1 << 23
+    a, b = 0x3C3C2323, 0x1717
+    E = rand_scalars_np(cv, n, 2323 + cid)
+    pos = 0
+    for g, size in enumerate((2000, 3800, 4096, 4200, 5000, 8000, 12000)):
+        E[pos:pos + size] = rand_scalars_np(cv, 1, 9100 + g)[0]
+        pos += size
+    d_b = ecgpu.gen_bases_dev(prog, cname, a, b, n)
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    out = ecgpu.msm_dev(prog, cname, d_b, d_e, n)
+    d_b.free()
+    d_e.free()
+    assert normalised_form_ok(cid, out)
+    assert same_point(cid, out, co.gen_mul(cid, co.kat_scalar(cid, a, b, E, nthreads=16)))
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
 def test_msm_record_runs_around_short_threshold(gpu_programs, cname, cid):
     """Groups of equal scalars whose buckets hold 900-3000 terms in every
     window: 7-24 accumulation segments, i.e. record runs on both sides of
