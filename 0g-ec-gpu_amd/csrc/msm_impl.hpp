@@ -699,17 +699,14 @@ struct LdsPoint {  // XYZZ<F> words of lane t at w[i * MSM_THREADS + t]
 // Several bucket arrays (slots, `slot_stride` buckets apart) hold the buckets
 // of the passes of one MSM (msm_host_t): bucket j is their sum, added into the
 // running sum slot by slot -- one reduction for every pass.
-// PM = 1: a lane pair per segment (pp_add), for launches under one wave per
-// SIMD (msm_tail_pairs).
-template <class F, int PM>
+template <class F>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
     msm_reduce_kernel(const XYZZ<F>* __restrict__ buckets, MsmPlan pl, XYZZ<F>* __restrict__ partial,
                       XYZZ<F>* __restrict__ runs, uint32_t slots, size_t slot_stride) {
   __shared__ uint32_t lds[LdsPoint<F>::NW * MSM_THREADS];
   const LdsPoint<F> acc_l{lds};
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t id = PM != 0 ? g >> 1 : g;
-  if (id >= pl.G * pl.S) return;  // both lanes of a pair leave together
+  const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= pl.G * pl.S) return;
   const uint32_t w = id / pl.S, sgm = id % pl.S;
   const XYZZ<F>* bk = buckets + (size_t)w * pl.B + (size_t)sgm * pl.LS;
   const uint32_t len = min(pl.LS, pl.B - sgm * pl.LS);  // the last segment may be shorter
@@ -717,14 +714,12 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
   acc_l.put(xyzz_zero<F>());
   for (int j = (int)len - 1; j >= 0; j--) {
 #pragma unroll 1
-    for (uint32_t q = 0; q < slots; q++) run = pp_add<PM>(run, load_xyzz(&bk[q * slot_stride + j]));
-    acc_l.put(pp_add<PM>(acc_l.get(), run));
+    for (uint32_t q = 0; q < slots; q++) run = pa_add(run, load_xyzz(&bk[q * slot_stride + j]));
+    acc_l.put(pa_add(acc_l.get(), run));
   }
   // acc = sum_j (j+1) S_j ; run = sum_j S_j
-  if (PM == 0 || (g & 1u) == 0) {
-    store_xyzz(&partial[id], acc_l.get());
-    store_xyzz(&runs[id], run);
-  }
+  store_xyzz(&partial[id], acc_l.get());
+  store_xyzz(&runs[id], run);
 }
 
 // partial[id] += (sgm LS) run_sgm  (segment offset of the bucket weights)
@@ -817,65 +812,45 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
 //     K serially per thread, then log2(256) LDS levels.  Every add here waits
 //     for the previous one (~15 us for a full add at this occupancy), so the
 //     launch is sized by K (offset_bits_k) to ~one workgroup per CU.
-//     PM = 1: lane pairs (pp_add), MSM_THREADS / 2 per workgroup; the lead
-//     lane of a pair writes its LDS slot.
-template <class F, int PM>
+//     Lane pairs (pp_add) were measured here and do not pay: 0.36 ms single
+//     lanes against 0.38 + 0.03 ms paired at 2^20 (profiles/r04/tail_pairs_trace.txt).
+template <class F>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
     msm_offset_bits_kernel(const XYZZ<F>* __restrict__ partial, const XYZZ<F>* __restrict__ runs, uint32_t S,
                            uint32_t KB, uint32_t K, uint32_t wgs, XYZZ<F>* __restrict__ out) {
   extern __shared__ uint32_t lds_pts[];
   const LdsPoints<F> pts{lds_pts};
-  constexpr uint32_t PB = PM != 0 ? 1u : 0u;
-  constexpr uint32_t NT = MSM_THREADS >> PB;  // operation lanes (pairs) per workgroup
-  const uint32_t g = blockIdx.x / wgs, b = blockIdx.x % wgs, t = threadIdx.x >> PB;
-  const bool lead = PM == 0 || (threadIdx.x & 1u) == 0;
+  const uint32_t g = blockIdx.x / wgs, b = blockIdx.x % wgs, t = threadIdx.x;
   const uint32_t w = g / (KB + 1), k = g % (KB + 1);
   const bool a_sum = k == KB;
   const XYZZ<F>* src = (a_sum ? partial : runs) + (size_t)w * S;
   const uint32_t cnt = a_sum ? S : (1u << (KB - 1));
-  const uint32_t span = NT * K;
+  const uint32_t span = MSM_THREADS * K;
   if (b * span >= cnt) {  // this group has fewer inputs than the widest one: the identity
-    if (threadIdx.x == 0) store_xyzz(&out[blockIdx.x], xyzz_zero<F>());
+    if (t == 0) store_xyzz(&out[blockIdx.x], xyzz_zero<F>());
     return;
   }
-  const uint32_t j0 = (b * NT + t) * K;
+  const uint32_t j0 = (b * MSM_THREADS + t) * K;
   XYZZ<F> acc = xyzz_zero<F>();
 #pragma unroll 1
   for (uint32_t q = 0; q < K; q++) {
     const uint32_t i = j0 + q;
     if (i >= cnt) break;
     const uint32_t sg = a_sum ? i : (((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1)));
-    if (sg < S) acc = pp_add<PM>(acc, load_xyzz(&src[sg]));
+    if (sg < S) acc = pa_add(acc, load_xyzz(&src[sg]));
   }
-  if (lead) pts.put(t, acc);
+  pts.put(t, acc);
   __syncthreads();
   const uint32_t left = cnt - b * span;
-  const uint32_t active = left >= span ? NT : (left + K - 1) / K;
+  const uint32_t active = left >= span ? MSM_THREADS : (left + K - 1) / K;
   uint32_t top = 1;
   while (top < active) top <<= 1;
 #pragma unroll 1
   for (uint32_t stride = top / 2; stride > 0; stride >>= 1) {
-    // a pair reads slots t and t + stride before its lead lane writes slot t
-    // (LDS operations of one wave complete in order); no other pair touches
-    // slot t at this level
-    if (t < stride) {
-      const XYZZ<F> v = pp_add<PM>(pts.get(t), pts.get(t + stride));
-      if (lead) pts.put(t, v);
-    }
+    if (t < stride) pts.put(t, pa_add(pts.get(t), pts.get(t + stride)));
     __syncthreads();
   }
-  if (threadIdx.x == 0) store_xyzz(&out[blockIdx.x], pts.get(0));
-}
-
-// Lane pairs in the reduction tail (A/B: ECG_MSM_TAIL_PAIRS, a bit mask:
-// 1 = offset-bit sums, 2 = running sums of launches at or under half a wave
-// per SIMD).  A pair pays off only while the paired launch still leaves each
-// SIMD at most one wave: from one wave to two, the extra exchange and select
-// instructions cost what the shorter chains save (EC-FFT 2^16: 26.6 -> 33.6
-// ms, profiles/r04/lane_pairs_ab.txt).
-static uint32_t msm_tail_pairs() {
-  static const uint32_t v = env_u32("ECG_MSM_TAIL_PAIRS", 1);
-  return v;
+  if (t == 0) store_xyzz(&out[blockIdx.x], pts.get(0));
 }
 
 static uint32_t offset_bits(uint32_t S) {  // KB of msm_offset_bits_kernel
@@ -1331,19 +1306,8 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
 
   void* runs;
   ECG_TRY(ws_get(ctx, "msm_runs", (size_t)pl.G * pl.S * sizeof(X), &runs));
-  // lane pairs where the launch leaves a SIMD one wave or less (msm_tail_pairs)
-  const bool tail_pairs = PairOps<F>::ok && (msm_tail_pairs() & 1u);
-  bool red_paired = false;
-  if constexpr (PairOps<F>::ok) {
-    if ((msm_tail_pairs() & 2u) && (size_t)pl.G * pl.S <= MSM_RED_THREADS / 4) {
-      hipLaunchKernelGGL((msm_reduce_kernel<F, 1>), dim3(blocks_for(2 * (size_t)pl.G * pl.S, MSM_THREADS)),
-                         dim3(MSM_THREADS), 0, s, (const X*)bk_all, pl, (X*)pa, (X*)runs, nslots, (size_t)nb);
-      red_paired = true;
-    }
-  }
-  if (!red_paired)
-    hipLaunchKernelGGL((msm_reduce_kernel<F, 0>), dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
-                       dim3(MSM_THREADS), 0, s, (const X*)bk_all, pl, (X*)pa, (X*)runs, nslots, (size_t)nb);
+  hipLaunchKernelGGL(msm_reduce_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
+                     dim3(MSM_THREADS), 0, s, (const X*)bk_all, pl, (X*)pa, (X*)runs, nslots, (size_t)nb);
   ECG_HIP(hipGetLastError());
   uint32_t cnt = pl.S;
   uint32_t groups = pl.G;
@@ -1353,28 +1317,18 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   if (tree_lds > 64 * 1024) {  // G2 points (96 KiB per workgroup) need the opt-in
     ECG_HIP(hipFuncSetAttribute((const void*)msm_tree_sum_kernel<F>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)tree_lds));
-    ECG_HIP(hipFuncSetAttribute((const void*)msm_offset_bits_kernel<F, 0>,
+    ECG_HIP(hipFuncSetAttribute((const void*)msm_offset_bits_kernel<F>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)tree_lds));
   }
   if (bits) {
     const uint32_t kb = offset_bits(pl.S);
     const uint32_t K = offset_bits_k(pl.S);
-    const uint32_t nt = tail_pairs ? MSM_THREADS / 2 : MSM_THREADS;  // operation lanes per workgroup
-    const uint32_t wgs = (pl.S + nt * K - 1) / (nt * K);
+    const uint32_t wgs = (pl.S + MSM_THREADS * K - 1) / (MSM_THREADS * K);
     groups = pl.G * (kb + 1);
     void* pbits;
     ECG_TRY(ws_get(ctx, "msm_pbits", (size_t)groups * wgs * sizeof(X), &pbits));
-    bool bits_paired = false;
-    if constexpr (PairOps<F>::ok) {
-      if (tail_pairs) {
-        hipLaunchKernelGGL((msm_offset_bits_kernel<F, 1>), dim3(groups * wgs), dim3(MSM_THREADS), tree_lds, s,
-                           (const X*)pa, (const X*)runs, pl.S, kb, K, wgs, (X*)pbits);
-        bits_paired = true;
-      }
-    }
-    if (!bits_paired)
-      hipLaunchKernelGGL((msm_offset_bits_kernel<F, 0>), dim3(groups * wgs), dim3(MSM_THREADS), tree_lds, s,
-                         (const X*)pa, (const X*)runs, pl.S, kb, K, wgs, (X*)pbits);
+    hipLaunchKernelGGL(msm_offset_bits_kernel<F>, dim3(groups * wgs), dim3(MSM_THREADS), tree_lds, s, (const X*)pa,
+                       (const X*)runs, pl.S, kb, K, wgs, (X*)pbits);
     ECG_HIP(hipGetLastError());
     in = (X*)pbits;
     cnt = wgs;
