@@ -329,6 +329,108 @@ ECG_DEV XYZZ<FpR<Q>> rr_add_x2(const XYZZ<FpR<Q>>& p, const XYZZ<FpR<Q>>& q) {
   return o;
 }
 
+// Quad forms: four lanes (threadIdx & 3) share each operation, one product
+// per lane and level, every level's results broadcast to the quad by DPP.
+// Per lane a doubling issues 1 squaring + 1 product + 1 product sum (pairs: 1
+// + 2 + 1; one lane: 9 products), a full add 3 products + 1 product sum
+// (pairs: 6 + 1; one lane: 14).  Same values and bounds as rr_dbl /
+// rr_add_xyzz; quad-uniform control flow.
+template <int L, class Q>
+ECG_DEV FpR<Q> rr_quad_bcast(const FpR<Q>& a) {  // lane L's value on every lane of the quad
+  constexpr int ctrl = L | (L << 2) | (L << 4) | (L << 6);  // quad_perm [L, L, L, L]
+  FpR<Q> r;
+#pragma unroll
+  for (int i = 0; i < Q::NL; i++) r.v[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.v[i], ctrl, 0xF, 0xF, false);
+  return r;
+}
+template <class Q>
+ECG_DEV FpR<Q> rr_pick4(uint32_t q, const FpR<Q>& a0, const FpR<Q>& a1, const FpR<Q>& a2, const FpR<Q>& a3) {
+  return rr_pick((q & 2) != 0, rr_pick((q & 1) != 0, a3, a2), rr_pick((q & 1) != 0, a1, a0));
+}
+
+// 2 P on a quad.  Lanes 0 / 1 / 2 / 3:
+//   level 1: V = U^2 | X2 = X^2 | (V) | (X2)
+//   level 2: W = U V | S = X V | ZZ3 = V ZZ | M^2
+//   level 3: ZZZ3 = W ZZZ | Y3 = M (S - X3) + Y (k p - W) | (ZZZ3) | (Y3)
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> rr_dbl_x4(const XYZZ<FpR<Q>>& p) {
+  using F = FpR<Q>;
+  if (xyzz_is_zero_rr(p)) return p;
+  const uint32_t q = threadIdx.x & 3u;
+  const bool odd = (q & 1u) != 0;
+  const F U = rr_add(p.Y, p.Y);
+  const F L1 = rr_sqr(rr_pick(odd, p.X, U));
+  const F V = rr_quad_bcast<0>(L1), X2 = rr_quad_bcast<1>(L1);
+  const F Mm = rr_add(rr_add(X2, X2), X2);
+  const F a = rr_mul(rr_pick4(q, U, p.X, V, Mm), rr_pick4(q, V, V, p.ZZ, Mm));
+  const F W = rr_quad_bcast<0>(a), S = rr_quad_bcast<1>(a), ZZ3 = rr_quad_bcast<2>(a), M2 = rr_quad_bcast<3>(a);
+  F X3, D;
+  if constexpr (rr_tight<Q>()) {
+    X3 = rr_reduce_q(rr_sub2<16>(M2, S, S));
+    D = rr_sub<4>(S, X3);
+  } else {
+    X3 = rr_sub2<16>(M2, S, S);
+    D = rr_sub<64>(S, X3);
+  }
+  const F z = F::zero();
+  const F r = rr_mul_sum2(rr_pick(odd, Mm, W), rr_pick(odd, D, p.ZZZ), rr_pick(odd, p.Y, z), rr_pick(odd, rr_neg<4>(W), z));
+  XYZZ<F> o;
+  o.X = X3;
+  o.Y = rr_quad_bcast<1>(r);
+  o.ZZ = ZZ3;
+  o.ZZZ = rr_quad_bcast<0>(r);
+  return o;
+}
+
+// P + Q on a quad.  Lanes 0 / 1 / 2 / 3:
+//   level 1: U1 = X1 ZZ2 | U2 = X2 ZZ1 | S1 = Y1 ZZZ2 | S2 = Y2 ZZZ1
+//   level 2: PP = P^2 | RR = R^2 | ZZ12 | ZZZ12
+//   level 3: PPP = P PP | Q = U1 PP | ZZ3 = ZZ12 PP | (ZZ3)
+//   level 4: Y3 = R (Q - X3) + S1 (k p - PPP) | ZZZ3 = ZZZ12 PPP | (Y3) | (ZZZ3)
+template <class Q>
+ECG_DEV XYZZ<FpR<Q>> rr_add_x4(const XYZZ<FpR<Q>>& p, const XYZZ<FpR<Q>>& q2) {
+  using F = FpR<Q>;
+  const bool pz = xyzz_is_zero_rr(p), qz = xyzz_is_zero_rr(q2);
+  XYZZ<F> o;
+  if (pz || qz) {
+    o = q2;
+    rr_sel(o, qz, p);
+    return o;
+  }
+  const uint32_t q = threadIdx.x & 3u;
+  const bool odd = (q & 1u) != 0;
+  const F a = rr_mul(rr_pick4(q, p.X, q2.X, p.Y, q2.Y), rr_pick4(q, q2.ZZ, p.ZZ, q2.ZZZ, p.ZZZ));
+  const F U1 = rr_quad_bcast<0>(a), U2 = rr_quad_bcast<1>(a), S1 = rr_quad_bcast<2>(a), S2 = rr_quad_bcast<3>(a);
+  const F P = rr_sub<4>(U2, U1);
+  const F R = rr_sub<4>(S2, S1);
+  const F b = rr_mul(rr_pick4(q, P, R, p.ZZ, p.ZZZ), rr_pick4(q, P, R, q2.ZZ, q2.ZZZ));
+  const F PP = rr_quad_bcast<0>(b), RR = rr_quad_bcast<1>(b), ZZ12 = rr_quad_bcast<2>(b), ZZZ12 = rr_quad_bcast<3>(b);
+  const F c = rr_mul(rr_pick4(q, P, U1, ZZ12, ZZ12), PP);
+  const F PPP = rr_quad_bcast<0>(c), Qv = rr_quad_bcast<1>(c);
+  F X3, D;
+  if constexpr (rr_tight<Q>()) {
+    X3 = rr_reduce_q(rr_sub3<16>(RR, PPP, Qv, Qv));
+    D = rr_sub<4>(Qv, X3);
+  } else {
+    X3 = rr_sub3<16>(RR, PPP, Qv, Qv);
+    D = rr_sub<64>(Qv, X3);
+  }
+  const F z = F::zero();
+  const F r = rr_mul_sum2(rr_pick(odd, ZZZ12, R), rr_pick(odd, PPP, D), rr_pick(odd, z, S1), rr_pick(odd, z, rr_neg<4>(PPP)));
+  o.X = X3;
+  o.Y = rr_quad_bcast<0>(r);
+  o.ZZ = rr_quad_bcast<2>(c);
+  o.ZZZ = rr_quad_bcast<1>(r);
+  if (rr_maybe_zero_prod(PP)) {  // rare, quad-uniform: P = Q or P = -Q
+    const bool inf = rr_is_zero_prod(PP);
+    const bool dbl = inf && rr_is_zero_prod(RR);
+    XYZZ<F> d = xyzz_zero<F>();
+    if (dbl) d = rr_dbl_x4(p);
+    rr_sel(o, inf, d);
+  }
+  return o;
+}
+
 // lane-pair forms exist for the reduced-radix G1 points
 template <class PF>
 struct PairOps {
@@ -372,17 +474,26 @@ ECG_DEV XYZZ<FpR<Q>> pa_dbl(const XYZZ<FpR<Q>>& p) {
 }
 
 // Point operations of latency-bound chains: one lane per operation (PM = 0),
-// or a lane pair (lanes ^ PM) sharing each operation's products
+// a lane pair (lanes ^ PM, PM = 1 or 2) or a quad (PM = 4, lanes & 3)
+// sharing each operation's products
+template <int PM>
+constexpr uint32_t pp_lanes_log() {
+  return PM == 0 ? 0u : PM == 4 ? 2u : 1u;
+}
 template <int PM, class PF>
 ECG_DEV XYZZ<PF> pp_dbl(const XYZZ<PF>& p) {
-  if constexpr (PM != 0)
+  if constexpr (PM == 4)
+    return rr_dbl_x4(p);
+  else if constexpr (PM != 0)
     return rr_dbl_x2<PM>(p);
   else
     return pa_dbl(p);
 }
 template <int PM, class PF>
 ECG_DEV XYZZ<PF> pp_add(const XYZZ<PF>& p, const XYZZ<PF>& q) {
-  if constexpr (PM != 0)
+  if constexpr (PM == 4)
+    return rr_add_x4(p, q);
+  else if constexpr (PM != 0)
     return rr_add_x2<PM>(p, q);
   else
     return pa_add(p, q);

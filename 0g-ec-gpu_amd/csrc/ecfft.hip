@@ -297,21 +297,22 @@ ECG_DEV XYZZ<PF> win_mul(const XYZZ<PF>& P, const uint32_t* k, XYZZ<PF>* __restr
 
 // Stage s (as ecfft_stage_kernel) with windowed products; GLV curves: lanes
 // 2u, 2u + 1 share butterfly u (half 0: k1 P, half 1: k2 phi(P)).  With PM = 1
-// every lane of that layout becomes a lane pair (lanes 2v, 2v + 1) sharing
-// each point operation's products (pp_dbl / pp_add): 4 lanes per butterfly on
-// GLV curves, 2 otherwise, and the GLV partner is lane ^ 2.
+// every lane of that layout becomes a lane pair (lanes 2v, 2v + 1), with PM = 4
+// a quad (lanes 4v .. 4v + 3), sharing each point operation's products
+// (pp_dbl / pp_add); the GLV partner is then lane ^ 2 or lane ^ 4.
 template <class C, class PF, int PM>
 __global__ void __launch_bounds__(ECFFT_THREADS)
     ecfft_stage_win_kernel(XYZZ<PF>* __restrict__ a, const uint4* __restrict__ tw, uint32_t log_n, uint32_t s,
                            uint32_t batch, XYZZ<PF>* __restrict__ tabs) {
   constexpr bool glv = has_glv<C>();
-  constexpr uint32_t PB = PM != 0 ? 1u : 0u;  // log2 lanes per point operation
+  constexpr uint32_t PB = pp_lanes_log<PM>();  // log2 lanes per point operation
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lanes_log = (glv ? log_n : log_n - 1) + PB;  // lanes per transform
   if (g >= (batch << lanes_log)) return;               // the lanes of a butterfly leave together
   a += (size_t)(g >> lanes_log) << log_n;              // transform g >> lanes_log of the batch
   const uint32_t gl = (g & ((1u << lanes_log) - 1)) >> PB;
-  const bool lead = PM == 0 || (g & 1u) == 0;          // the lane of a pair that stores
+  const uint32_t role = g & ((1u << PB) - 1);           // lane within the point operation
+  const bool lead = role == 0;                          // the lane that stores
   const uint32_t t = glv ? gl >> 1 : gl;
   const uint32_t half = glv ? (gl & 1) : 0u;
   const uint32_t h = 1u << s;
@@ -340,20 +341,20 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
   if constexpr (glv) {  // half 0 writes A + wB, half 1 A - wB
     const XYZZ<PF> o = pp_add<PM>(A, neg_if(R, half != 0));
     if (lead) store_xyzz(&a[half ? i1 : i0], o);
-  } else if constexpr (PM != 0) {  // the pair's lanes store one output each
+  } else if constexpr (PM != 0) {  // lanes 0 and 1 of the operation store one output each
     const XYZZ<PF> o0 = pp_add<PM>(A, R);
     const XYZZ<PF> o1 = pp_add<PM>(A, pa_neg(R));
-    store_xyzz(&a[lead ? i0 : i1], lead ? o0 : o1);
+    if (role < 2) store_xyzz(&a[lead ? i0 : i1], lead ? o0 : o1);
   } else {
     store_xyzz(&a[i0], pa_add(A, R));
     store_xyzz(&a[i1], pa_add(A, pa_neg(R)));
   }
 }
 
-static bool ecfft_pairs_enabled() {  // A/B switch: ECG_ECFFT_PAIRS=0 keeps one lane per point operation
-  static const bool v = [] {
+static uint32_t ecfft_pairs_max() {  // A/B: ECG_ECFFT_PAIRS = 0 / 1 (single lanes), 2 (pairs), 4 (quads)
+  static const uint32_t v = [] {
     const char* e = getenv("ECG_ECFFT_PAIRS");
-    return !(e && e[0] == '0');
+    return e ? (uint32_t)strtoul(e, nullptr, 10) : 4u;
   }();
   return v;
 }
@@ -408,14 +409,17 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
   void *a, *tw, *gt = nullptr;
   ECG_TRY(ws_get(ctx, "ecfft_pts", nb * sizeof(XYZZ<PF>), &a));
   ECG_TRY(ws_get(ctx, "ecfft_tw", (size_t)(n / 2 + 1) * 32, &tw));
-  // lane pairs while the paired stage still leaves each SIMD at most one
-  // wave (2^15 lanes before pairing): 2^10-2^14 G1 stages 33 % faster; at
-  // 2^16 (one wave per SIMD unpaired) pairs are 26 % slower
-  // (profiles/r04/lane_pairs_ab.txt)
+  // lane pairs / quads while the widened stage still leaves each SIMD at most
+  // one wave (2^16 lanes): pairs made 2^10-2^14 G1 stages 33 % faster, but at
+  // 2^16 (one wave per SIMD unpaired) they are 26 % slower
+  // (profiles/r04/lane_pairs_ab.txt).  ECG_ECFFT_PAIRS: 0 single lanes,
+  // 2 pairs at most, 4 (default) quads where they fit.
   const size_t lanes1 = has_glv<C>() && win ? nb : (size_t)batch * (n / 2);
-  const bool pairs = win && PairOps<PF>::ok && ecfft_pairs_enabled() && lanes1 <= ((size_t)1 << 15);
-  // stage lanes: 2 per butterfly on GLV curves, doubled by lane pairs
-  const size_t lanes = (lanes1 << (pairs ? 1 : 0)) + 1;
+  const uint32_t pmax = win && PairOps<PF>::ok ? ecfft_pairs_max() : 1u;
+  const uint32_t widen = pmax >= 4 && lanes1 <= ((size_t)1 << 14) ? 4u : pmax >= 2 && lanes1 <= ((size_t)1 << 15) ? 2u : 1u;
+  const bool pairs = widen > 1;
+  // stage lanes: 2 per butterfly on GLV curves, times the lanes per operation
+  const size_t lanes = lanes1 * widen + 1;
   if (win)
     ECG_TRY(ws_get(ctx, "ecfft_tab", lanes * ECFFT_TAB * sizeof(XYZZ<PF>), &gt));
   else if (has_glv<C>())
@@ -439,7 +443,12 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
     ECG_TRY(kt_begin(ctx, "ecfft_stage", s));
     if constexpr (!std::is_same<PF, F>::value) {
       const size_t stage_lanes = has_glv<C>() ? nb : nb / 2;
-      if (win && pairs) {
+      if (win && widen == 4) {
+        if constexpr (PairOps<PF>::ok)
+          hipLaunchKernelGGL((ecfft_stage_win_kernel<C, PF, 4>), dim3(ecfft_blocks(4 * stage_lanes)),
+                             dim3(ECFFT_THREADS), 0, s, (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, batch,
+                             (XYZZ<PF>*)gt);
+      } else if (win && pairs) {
         if constexpr (PairOps<PF>::ok)
           hipLaunchKernelGGL((ecfft_stage_win_kernel<C, PF, 1>), dim3(ecfft_blocks(2 * stage_lanes)),
                              dim3(ECFFT_THREADS), 0, s, (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, batch,

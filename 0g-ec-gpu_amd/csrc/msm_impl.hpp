@@ -949,25 +949,26 @@ __global__ void msm_sums_to_std_kernel(const XYZZ<F>* __restrict__ in, uint32_t 
 // Batched form: the per-task Horner over its W window sums in the pipeline's
 // reduced-radix point form, before the conversion.  The fold is a
 // latency-bound chain of c (W - 1) doublings -- 1024 tasks are 16 waves on
-// 1024 SIMDs, each wave alone on its SIMD -- so on G1 a lane pair takes each
-// task (PM = 1: pp_dbl / pp_add share every operation's products) and a wave
-// issues about half the instructions per doubling.
+// 1024 SIMDs, each wave alone on its SIMD -- so on G1 a lane quad (PM = 4)
+// or pair (PM = 1) takes each task: pp_dbl / pp_add share every operation's
+// products and a wave issues fewer instructions per doubling.
 template <class F, int PM>
 __global__ void __launch_bounds__(64)
     msm_fold_rr_kernel(const XYZZ<F>* __restrict__ sums, uint32_t nw, uint32_t c, uint32_t tasks,
                        XYZZ<F>* __restrict__ out) {
+  constexpr uint32_t PB = pp_lanes_log<PM>();
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t t = PM != 0 ? g >> 1 : g;
-  if (t >= tasks) return;  // both lanes of a pair leave together
+  const uint32_t t = g >> PB;
+  if (t >= tasks) return;  // the lanes of a task leave together
   XYZZ<F> acc = load_xyzz(&sums[(size_t)t * nw + nw - 1]);
   for (int w = (int)nw - 2; w >= 0; w--) {
     for (uint32_t k = 0; k < c; k++) acc = pp_dbl<PM>(acc);
     acc = pp_add<PM>(acc, load_xyzz(&sums[(size_t)t * nw + w]));
   }
-  if (PM == 0 || (g & 1u) == 0) store_xyzz(&out[t], acc);
+  if ((g & ((1u << PB) - 1)) == 0) store_xyzz(&out[t], acc);
 }
-static bool msm_fold_pairs_enabled() {  // A/B switch: ECG_MSM_FOLD_PAIRS=0 keeps one lane per task
-  static const bool v = env_u32("ECG_MSM_FOLD_PAIRS", 1) != 0;
+static uint32_t msm_fold_lanes() {  // A/B: ECG_MSM_FOLD_PAIRS = 0 / 1 (one lane per task), 2 (pairs), 4 (quads)
+  static const uint32_t v = env_u32("ECG_MSM_FOLD_PAIRS", 4);
   return v;
 }
 
@@ -1364,9 +1365,14 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     uint32_t npts = pl.G;
     if (folded && pl.fold_windows() > 1 && ECG_MSM_FOLD_RR_ON) {  // batched: Horner per task first
       const uint32_t tasks = pl.G / pl.W;
+      // lane quads / pairs while they leave each SIMD at most one wave
       bool paired = false;
       if constexpr (PairOps<F>::ok) {
-        if (msm_fold_pairs_enabled()) {
+        if (msm_fold_lanes() >= 4 && tasks <= (1u << 14)) {
+          hipLaunchKernelGGL((msm_fold_rr_kernel<F, 4>), dim3(blocks_for(4 * (size_t)tasks, 64)), dim3(64), 0, s,
+                             (const X*)in, pl.W, pl.c, tasks, out);
+          paired = true;
+        } else if (msm_fold_lanes() >= 2 && tasks <= (1u << 15)) {
           hipLaunchKernelGGL((msm_fold_rr_kernel<F, 1>), dim3(blocks_for(2 * (size_t)tasks, 64)), dim3(64), 0, s,
                              (const X*)in, pl.W, pl.c, tasks, out);
           paired = true;
