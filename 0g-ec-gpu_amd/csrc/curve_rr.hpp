@@ -431,13 +431,22 @@ ECG_DEV XYZZ<FpR<Q>> rr_add_x4(const XYZZ<FpR<Q>>& p, const XYZZ<FpR<Q>>& q2) {
   return o;
 }
 
-// lane-pair forms exist for the reduced-radix G1 points
+// lane-pair forms exist for the reduced-radix G1 points (and, curve_rr2.hpp,
+// G2); quads for G1
 template <class PF>
 struct PairOps {
   static constexpr bool ok = false;
 };
 template <class Q>
 struct PairOps<FpR<Q>> {
+  static constexpr bool ok = true;
+};
+template <class PF>
+struct QuadOps {
+  static constexpr bool ok = false;
+};
+template <class Q>
+struct QuadOps<FpR<Q>> {
   static constexpr bool ok = true;
 };
 

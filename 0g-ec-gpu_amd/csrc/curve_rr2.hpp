@@ -225,6 +225,87 @@ ECG_DEV XYZZ<FpR2<Q>> r2_add_xyzz(const XYZZ<FpR2<Q>>& p, const XYZZ<FpR2<Q>>& q
 }
 
 // ---------------------------------------------------------------------------
+// Lane-pair forms (curve_rr.hpp rr_dbl_x2's role for G2): every Fq2 product
+// is two independent component product sums, so each lane of the pair
+// (lanes ^ M) computes one component -- lo c0, hi c1 -- and the pair swaps
+// them.  Same formulas, values and bounds as r2_dbl / r2_add_xyzz; half the
+// product instructions per lane.  Pair-uniform control flow.
+// ---------------------------------------------------------------------------
+template <int M, class Q>
+ECG_DEV FpR2<Q> r2_join(const FpR<Q>& mine) {  // (c0, c1) from each lane's component
+  const bool h = pair_hi<M>();
+  const FpR<Q> other = rr_lane_swap<M>(mine);
+  return mkr2(rr_pick(h, other, mine), rr_pick(h, mine, other));
+}
+template <int M, int K, class Q>
+ECG_DEV FpR2<Q> r2_mul_x2(const FpR2<Q>& a, const FpR2<Q>& b) {
+  const bool h = pair_hi<M>();
+  return r2_join<M>(rr_mul_sum2(a.c0, rr_pick(h, b.c1, b.c0), a.c1, rr_pick(h, b.c0, rr_neg<K>(b.c1))));
+}
+template <int M, int K, class Q>
+ECG_DEV FpR2<Q> r2_sqr_x2(const FpR2<Q>& a) {
+  const bool h = pair_hi<M>();
+  return r2_join<M>(rr_mul(rr_pick(h, rr_add(a.c0, a.c0), rr_add(a.c0, a.c1)), rr_pick(h, a.c1, rr_sub<K>(a.c0, a.c1))));
+}
+
+template <int M, class Q>
+ECG_DEV XYZZ<FpR2<Q>> rr_dbl_x2(const XYZZ<FpR2<Q>>& p) {
+  using F = FpR2<Q>;
+  if (fis_zero(p.ZZ)) return p;
+  XYZZ<F> r;
+  const F U = r2_add(p.Y, p.Y);
+  const F V = r2_sqr_x2<M, 64>(U);
+  const F X2 = r2_sqr_x2<M, 64>(p.X);
+  const F W = r2_mul_x2<M, 4>(U, V);
+  const F S = r2_mul_x2<M, 4>(p.X, V);
+  const F Mm = r2_add(r2_add(X2, X2), X2);
+  r.X = r2_sub2<16>(r2_sqr_x2<M, 8>(Mm), S, S);
+  r.Y = r2_add(r2_mul_x2<M, 8>(r2_sub<64>(S, r.X), Mm), r2_mul_x2<M, 8>(p.Y, r2_neg<4>(W)));
+  r.ZZ = r2_mul_x2<M, 4>(p.ZZ, V);
+  r.ZZZ = r2_mul_x2<M, 4>(p.ZZZ, W);
+  return r;
+}
+
+template <int M, class Q>
+ECG_DEV XYZZ<FpR2<Q>> rr_add_x2(const XYZZ<FpR2<Q>>& p, const XYZZ<FpR2<Q>>& q) {
+  using F = FpR2<Q>;
+  const bool pz = fis_zero(p.ZZ), qz = fis_zero(q.ZZ);
+  XYZZ<F> r;
+  if (pz || qz) {
+    r = q;
+    rr_sel(r, qz, p);
+    return r;
+  }
+  const F U1 = r2_mul_x2<M, 4>(p.X, q.ZZ);
+  const F U2 = r2_mul_x2<M, 4>(q.X, p.ZZ);
+  const F S1 = r2_mul_x2<M, 4>(p.Y, q.ZZZ);
+  const F S2 = r2_mul_x2<M, 4>(q.Y, p.ZZZ);
+  const F P = r2_sub<4>(U2, U1);
+  const F R = r2_sub<4>(S2, S1);
+  const F PP = r2_sqr_x2<M, 16>(P);
+  const F RR = r2_sqr_x2<M, 16>(R);
+  const F PPP = r2_mul_x2<M, 4>(P, PP);
+  const F Qv = r2_mul_x2<M, 4>(U1, PP);
+  r.ZZ = r2_mul_x2<M, 4>(r2_mul_x2<M, 4>(p.ZZ, q.ZZ), PP);
+  r.ZZZ = r2_mul_x2<M, 4>(r2_mul_x2<M, 4>(p.ZZZ, q.ZZZ), PPP);
+  r.X = r2_sub3<16>(RR, PPP, Qv, Qv);
+  r.Y = r2_add(r2_mul_x2<M, 16>(r2_sub<64>(Qv, r.X), R), r2_mul_x2<M, 8>(S1, r2_neg<4>(PPP)));
+  if (r2_maybe_zero_prod(PP)) {  // pair-uniform: both lanes hold PP, RR
+    const bool inf = r2_is_zero_prod(PP);
+    const bool dbl = inf && r2_is_zero_prod(RR);
+    XYZZ<F> d = xyzz_zero<F>();
+    if (dbl) d = rr_dbl_x2<M>(p);
+    rr_sel(r, inf, d);
+  }
+  return r;
+}
+
+template <class Q>
+struct PairOps<FpR2<Q>> {
+  static constexpr bool ok = true;
+};
+
+// ---------------------------------------------------------------------------
 // point-arithmetic policy (curve_rr.hpp) for the Fq2 form
 // ---------------------------------------------------------------------------
 template <class Q>

@@ -416,7 +416,9 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
   // 2 pairs at most, 4 (default) quads where they fit.
   const size_t lanes1 = has_glv<C>() && win ? nb : (size_t)batch * (n / 2);
   const uint32_t pmax = win && PairOps<PF>::ok ? ecfft_pairs_max() : 1u;
-  const uint32_t widen = pmax >= 4 && lanes1 <= ((size_t)1 << 14) ? 4u : pmax >= 2 && lanes1 <= ((size_t)1 << 15) ? 2u : 1u;
+  const uint32_t widen = QuadOps<PF>::ok && pmax >= 4 && lanes1 <= ((size_t)1 << 14)  ? 4u
+                         : pmax >= 2 && lanes1 <= ((size_t)1 << 15)                 ? 2u
+                                                                                    : 1u;
   const bool pairs = widen > 1;
   // stage lanes: 2 per butterfly on GLV curves, times the lanes per operation
   const size_t lanes = lanes1 * widen + 1;
@@ -444,7 +446,7 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
     if constexpr (!std::is_same<PF, F>::value) {
       const size_t stage_lanes = has_glv<C>() ? nb : nb / 2;
       if (win && widen == 4) {
-        if constexpr (PairOps<PF>::ok)
+        if constexpr (QuadOps<PF>::ok)
           hipLaunchKernelGGL((ecfft_stage_win_kernel<C, PF, 4>), dim3(ecfft_blocks(4 * stage_lanes)),
                              dim3(ECFFT_THREADS), 0, s, (XYZZ<PF>*)a, (const uint4*)tw, log_n, st, batch,
                              (XYZZ<PF>*)gt);

@@ -812,8 +812,9 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
 //     K serially per thread, then log2(256) LDS levels.  Every add here waits
 //     for the previous one (~15 us for a full add at this occupancy), so the
 //     launch is sized by K (offset_bits_k) to ~one workgroup per CU.
-//     Lane pairs (pp_add) were measured here and do not pay: 0.36 ms single
-//     lanes against 0.38 + 0.03 ms paired at 2^20 (profiles/r04/tail_pairs_trace.txt).
+//     Lane pairs (pp_add) do not pay here, capped at 2 waves/SIMD of
+//     registers or not: 0.36 ms single against 0.38-0.41 ms paired at 2^20
+//     (profiles/r04/tail_pairs_trace.txt, bits_pairs_trace.txt).
 template <class F>
 __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
     msm_offset_bits_kernel(const XYZZ<F>* __restrict__ partial, const XYZZ<F>* __restrict__ runs, uint32_t S,
@@ -1367,12 +1368,15 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
       const uint32_t tasks = pl.G / pl.W;
       // lane quads / pairs while they leave each SIMD at most one wave
       bool paired = false;
-      if constexpr (PairOps<F>::ok) {
+      if constexpr (QuadOps<F>::ok) {
         if (msm_fold_lanes() >= 4 && tasks <= (1u << 14)) {
           hipLaunchKernelGGL((msm_fold_rr_kernel<F, 4>), dim3(blocks_for(4 * (size_t)tasks, 64)), dim3(64), 0, s,
                              (const X*)in, pl.W, pl.c, tasks, out);
           paired = true;
-        } else if (msm_fold_lanes() >= 2 && tasks <= (1u << 15)) {
+        }
+      }
+      if constexpr (PairOps<F>::ok) {
+        if (!paired && msm_fold_lanes() >= 2 && tasks <= (1u << 15)) {
           hipLaunchKernelGGL((msm_fold_rr_kernel<F, 1>), dim3(blocks_for(2 * (size_t)tasks, 64)), dim3(64), 0, s,
                              (const X*)in, pl.W, pl.c, tasks, out);
           paired = true;

@@ -110,6 +110,38 @@ def test_g2_ec_fft_linearity(gpu_programs, cname, cid, cv):
 
 
 @pytest.mark.parametrize("cname,cid,cv", G2)
+def test_g2_ec_fft_equal_and_alternating_points(gpu_programs, cname, cid, cv):
+    """All P_j = P: out_0 = n P and out_k = O for k != 0 (sum_j w^(jk) = 0);
+    P_j = (-1)^j P: out_(n/2) = n P, every other out_k = O.  Stage 0 adds P to
+    P and to -P, so the full add's doubling and identity branches run (on lane
+    pairs, curve_rr2.hpp rr_add_x2, at these sizes)."""
+    prog = gpu_programs[0][0]
+    p = cv.fq.modulus
+    r = cv.fr.modulus
+    k0 = 0xBEEF + cid
+    P = po.g2_scalar_mul(cv, cv.gen, k0)
+    Pa = po.g2_to_affine(cv, P)
+    one = fq2_limbs(cv, po.Fq2(1, 0, p))
+    row = np.array(fq2_limbs(cv, Pa[0]) + fq2_limbs(cv, Pa[1]) + one, dtype=np.uint64)
+    nrow = np.array(fq2_limbs(cv, Pa[0]) + fq2_limbs(cv, po.Fq2(0, 0, p) - Pa[1]) + one, dtype=np.uint64)
+    k = ecgpu.EcFftKernel.create([prog], cname)
+    for log_n in (1, 3, 6):
+        n = 1 << log_n
+        om = co.u64arr([cv.fr.to_mont(cv.fr.omega(n))], 4)[0]
+        nP = po.g2_to_affine(cv, po.g2_scalar_mul(cv, cv.gen, n * k0 % r))
+        for pattern, hot in (("equal", 0), ("alternating", n // 2)):
+            rows = [row if (pattern == "equal" or j % 2 == 0) else nrow for j in range(n)]
+            jac = np.ascontiguousarray(np.stack(rows))
+            k.radix_ec_fft(jac, om, log_n)
+            for kk in range(n):
+                got = to_py_affine(cv, jac[kk])
+                if kk == hot:
+                    assert got == nP, (log_n, pattern, kk)
+                else:
+                    assert got is None, (log_n, pattern, kk)
+
+
+@pytest.mark.parametrize("cname,cid,cv", G2)
 def test_g2_msm_exceptional_paths(gpu_programs, cname, cid, cv):
     """Equal bases drive the doubling branch of the mixed add (acc = P, + P)
     and of the full add in the combine / reduction (k P + k P); a base next to
