@@ -552,6 +552,19 @@ def main():
         ecgpu.ec_fft_dev(prog, args.curve, d_jac, om_e, le)
         ef_s = time.perf_counter() - t_a
         aux["ec_fft"] = {"log_n": le, "ms": ef_s * 1e3, "butterflies_per_s": (1 << (le - 1)) * le / ef_s}
+        # the smaller sizes 0g runs (2^10-2^14): point operations on lane quads / pairs
+        small = {}
+        for ls in (10, 12, 14):
+            ns = 1 << ls
+            d_s = ecgpu.DeviceBuffer.upload(prog, np.ascontiguousarray(jac[:ns]))
+            om_s = omega_for(cid, r_int, ls)
+            ecgpu.ec_fft_dev(prog, args.curve, d_s, om_s, ls)
+            d_s.write(np.ascontiguousarray(jac[:ns]))
+            t_a = time.perf_counter()
+            ecgpu.ec_fft_dev(prog, args.curve, d_s, om_s, ls)
+            small[str(ls)] = (time.perf_counter() - t_a) * 1e3
+            d_s.free()
+        aux["ec_fft_small_ms"] = small
         d_jac.free()
         d_pts.free()
         # radix_ec_fft_many over 16 same-size inputs (the 2^16 points cut into 2^12
@@ -590,6 +603,21 @@ def main():
                          "kat": bool(_g2_kat(cid, gs, r_int, out_g2))}
         d_gp.free()
         d_gs.free()
+        # G2 EC-FFT 2^12 (component-split lane pairs): device-resident Jacobian points
+        l2 = 12
+        lq2 = 2 * lq
+        aff2 = ecgpu.gen_bases_dev(prog, g2, 3, 7, 1 << l2).read(shape=(1 << l2, 2 * lq2))
+        one2 = np.zeros(lq2, dtype=np.uint64)
+        one2[:lq] = one
+        jac2 = np.ascontiguousarray(np.concatenate([aff2, np.tile(one2, (1 << l2, 1))], axis=1))
+        d_j2 = ecgpu.DeviceBuffer.upload(prog, jac2)
+        om_2 = omega_for(cid, r_int, l2)
+        ecgpu.ec_fft_dev(prog, g2, d_j2, om_2, l2)
+        d_j2.write(jac2)
+        t_a = time.perf_counter()
+        ecgpu.ec_fft_dev(prog, g2, d_j2, om_2, l2)
+        aux["g2_ec_fft"] = {"log_n": l2, "ms": (time.perf_counter() - t_a) * 1e3}
+        d_j2.free()
 
     if rank != 0:
         group.barrier()
