@@ -831,11 +831,14 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
     if (t == 0) store_xyzz(&out[blockIdx.x], xyzz_zero<F>());
     return;
   }
-  const uint32_t j0 = (b * MSM_THREADS + t) * K;
+  // input i = b span + q MSM_THREADS + t: a wave's lanes read neighbouring
+  // segments at every step (coalesced), where a run of K per thread had each
+  // lane stream its own region
+  const uint32_t j0 = b * span + t;
   XYZZ<F> acc = xyzz_zero<F>();
 #pragma unroll 1
   for (uint32_t q = 0; q < K; q++) {
-    const uint32_t i = j0 + q;
+    const uint32_t i = j0 + q * MSM_THREADS;
     if (i >= cnt) break;
     const uint32_t sg = a_sum ? i : (((i >> k) << (k + 1)) | (1u << k) | (i & ((1u << k) - 1)));
     if (sg < S) acc = pa_add(acc, load_xyzz(&src[sg]));
@@ -843,7 +846,7 @@ __global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
   pts.put(t, acc);
   __syncthreads();
   const uint32_t left = cnt - b * span;
-  const uint32_t active = left >= span ? MSM_THREADS : (left + K - 1) / K;
+  const uint32_t active = left >= MSM_THREADS ? MSM_THREADS : left;  // threads holding an input
   uint32_t top = 1;
   while (top < active) top <<= 1;
 #pragma unroll 1
