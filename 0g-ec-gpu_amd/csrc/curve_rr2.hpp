@@ -300,6 +300,105 @@ ECG_DEV XYZZ<FpR2<Q>> rr_add_x2(const XYZZ<FpR2<Q>>& p, const XYZZ<FpR2<Q>>& q) 
   return r;
 }
 
+// Quad forms for G2: lane bit 0 splits each Fq2 product's components (as
+// the pair forms above), lane bit 1 splits each level's products (as
+// curve_rr.hpp rr_dbl_x2<2> / rr_add_x2<2> on G1).  Each lane computes at most
+// two component product sums per level.  Same values and bounds as r2_dbl /
+// r2_add_xyzz (a square runs as a product; K is the larger of the two lanes'
+// negation bounds, well inside the 2^25 slack).  Quad-uniform control flow.
+template <int M, class Q>
+ECG_DEV FpR2<Q> r2_lane_swap(const FpR2<Q>& a) {
+  return mkr2(rr_lane_swap<M>(a.c0), rr_lane_swap<M>(a.c1));
+}
+template <class Q>
+ECG_DEV FpR2<Q> r2_pick(bool c, const FpR2<Q>& a, const FpR2<Q>& b) {
+  return mkr2(rr_pick(c, a.c0, b.c0), rr_pick(c, a.c1, b.c1));
+}
+
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> rr_dbl_x4(const XYZZ<FpR2<Q>>& p) {
+  using F = FpR2<Q>;
+  if (fis_zero(p.ZZ)) return p;
+  const bool h = pair_hi<2>();  // level role; the component role is bit 0
+  const F z = F::zero();
+  const F U = r2_add(p.Y, p.Y);
+  const F L1 = r2_mul_x2<1, 64>(r2_pick(h, p.X, U), r2_pick(h, p.X, U));  // lo V = U^2 | hi X2 = X^2
+  const F O1 = r2_lane_swap<2>(L1);
+  const F V = r2_pick(h, O1, L1), X2 = r2_pick(h, L1, O1);
+  const F Mm = r2_add(r2_add(X2, X2), X2);
+  const F a0 = r2_mul_x2<1, 4>(r2_pick(h, p.X, U), V);               // lo W = U V   | hi S = X V
+  const F a1 = r2_mul_x2<1, 8>(r2_pick(h, Mm, p.ZZ), r2_pick(h, Mm, V));  // lo ZZ3 = ZZ V | hi M^2
+  const F O2 = r2_lane_swap<2>(a0);
+  const F W = r2_pick(h, O2, a0), S = r2_pick(h, a0, O2);
+  const F X3 = r2_sub2<16>(a1, S, S);  // meaningful on the hi lanes
+  const F D = r2_sub<64>(S, X3);
+  // lo: ZZZ3 = ZZZ W | hi: Y3 = D M + Y (4p - W)
+  const F r = r2_add(r2_mul_x2<1, 8>(r2_pick(h, D, p.ZZZ), r2_pick(h, Mm, W)),
+                     r2_mul_x2<1, 8>(r2_pick(h, p.Y, z), r2_pick(h, r2_neg<4>(W), z)));
+  const F f = r2_lane_swap<2>(r);                   // lo <- Y3, hi <- ZZZ3
+  const F g = r2_lane_swap<2>(r2_pick(h, X3, a1));  // lo <- X3, hi <- ZZ3
+  XYZZ<F> o;
+  o.X = r2_pick(h, X3, g);
+  o.Y = r2_pick(h, r, f);
+  o.ZZ = r2_pick(h, g, a1);
+  o.ZZZ = r2_pick(h, f, r);
+  return o;
+}
+
+template <class Q>
+ECG_DEV XYZZ<FpR2<Q>> rr_add_x4(const XYZZ<FpR2<Q>>& p, const XYZZ<FpR2<Q>>& q) {
+  using F = FpR2<Q>;
+  const bool pz = fis_zero(p.ZZ), qz = fis_zero(q.ZZ);
+  XYZZ<F> o;
+  if (pz || qz) {
+    o = q;
+    rr_sel(o, qz, p);
+    return o;
+  }
+  const bool h = pair_hi<2>();
+  const F z = F::zero();
+  const F a0 = r2_mul_x2<1, 4>(r2_pick(h, q.X, p.X), r2_pick(h, p.ZZ, q.ZZ));    // lo U1 | hi U2
+  const F a1 = r2_mul_x2<1, 4>(r2_pick(h, q.Y, p.Y), r2_pick(h, p.ZZZ, q.ZZZ));  // lo S1 | hi S2
+  const F e0 = r2_lane_swap<2>(a0), e1 = r2_lane_swap<2>(a1);
+  const F U1 = r2_pick(h, e0, a0), U2 = r2_pick(h, a0, e0);
+  const F S1 = r2_pick(h, e1, a1), S2 = r2_pick(h, a1, e1);
+  const F P = r2_sub<4>(U2, U1);
+  const F R = r2_sub<4>(S2, S1);
+  const F b0 = r2_mul_x2<1, 16>(r2_pick(h, p.ZZ, P), r2_pick(h, q.ZZ, P));    // lo PP | hi ZZ12
+  const F b1 = r2_mul_x2<1, 16>(r2_pick(h, p.ZZZ, R), r2_pick(h, q.ZZZ, R));  // lo RR | hi ZZZ12
+  const F e2 = r2_lane_swap<2>(b0);
+  const F PP = r2_pick(h, e2, b0), ZZ12 = r2_pick(h, b0, e2);
+  const F c0 = r2_mul_x2<1, 4>(r2_pick(h, ZZ12, P), PP);   // lo PPP | hi ZZ3
+  const F c1 = r2_mul_x2<1, 4>(r2_pick(h, ZZ12, U1), PP);  // lo Q   | hi ZZ3
+  const F e3 = r2_lane_swap<2>(c0);
+  const F PPP = r2_pick(h, e3, c0), ZZ3 = r2_pick(h, c0, e3);
+  const F X3 = r2_sub3<16>(b1, PPP, c1, c1);  // meaningful on the lo lanes
+  const F D = r2_sub<64>(c1, X3);
+  // lo: Y3 = D R + S1 (4p - PPP) | hi: ZZZ3 = ZZZ12 PPP
+  const F r = r2_add(r2_mul_x2<1, 16>(r2_pick(h, b1, D), r2_pick(h, PPP, R)),
+                     r2_mul_x2<1, 8>(r2_pick(h, z, S1), r2_pick(h, z, r2_neg<4>(PPP))));
+  const F f = r2_lane_swap<2>(r);   // lo <- ZZZ3, hi <- Y3
+  const F g = r2_lane_swap<2>(X3);  // hi <- X3
+  o.X = r2_pick(h, g, X3);
+  o.Y = r2_pick(h, f, r);
+  o.ZZ = ZZ3;
+  o.ZZZ = r2_pick(h, r, f);
+  if (r2_maybe_zero_prod(PP)) {  // rare, quad-uniform (every lane holds PP)
+    const F RRv = r2_pick(h, r2_lane_swap<2>(b1), b1);
+    const bool inf = r2_is_zero_prod(PP);
+    const bool dbl = inf && r2_is_zero_prod(RRv);
+    XYZZ<F> d = xyzz_zero<F>();
+    if (dbl) d = rr_dbl_x4(p);
+    rr_sel(o, inf, d);
+  }
+  return o;
+}
+
+template <class Q>
+struct QuadOps<FpR2<Q>> {
+  static constexpr bool ok = true;
+};
+
 template <class Q>
 struct PairOps<FpR2<Q>> {
   static constexpr bool ok = true;
