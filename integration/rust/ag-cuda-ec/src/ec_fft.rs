@@ -4,7 +4,7 @@
 use ecgpu_sys as sys;
 
 use crate::pairing_suite::{Affine, Curve, Scalar};
-use crate::workspace::{check, curve_of, ActiveWorkspace, CudaResult};
+use crate::workspace::{check, curve_of, ActiveWorkspace, CudaError, CudaResult};
 use crate::{GLOBAL, LOCAL};
 
 /// `input` (2^k projective points) is replaced by its DFT at `omegas[0]`
@@ -16,6 +16,8 @@ pub fn radix_ec_fft(
     let log_n = n.ilog2();
     assert_eq!(n, 1 << log_n);
     let curve = curve_of::<Affine>()?;
+    // the engine reads and writes `Curve` as [X, Y, Z] in place
+    ecgpu_ark::require_projective_xyz::<Affine>().map_err(|m| CudaError::InvalidValue(m.into()))?;
     check(unsafe {
         sys::ecg_ec_fft(workspace.ctx(), curve, input.as_mut_ptr() as *mut u64,
                         omegas.as_ptr() as *const u64, log_n, None, std::ptr::null_mut())

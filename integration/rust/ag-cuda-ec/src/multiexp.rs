@@ -100,6 +100,8 @@ pub fn multiple_multiexp(
 ) -> CudaResult<Vec<Curve>> {
     let _ = (window_size, neg_is_cheap);
     let curve = curve_of::<Affine>()?;
+    // the engine writes its Jacobian [X, Y, Z] results into `Curve` in place
+    ecgpu_ark::require_projective_xyz::<Affine>().map_err(|m| CudaError::InvalidValue(m.into()))?;
     let num_lines = bases_gpu.len() / exponents.len();
     let mut output = vec![Curve::zero(); num_chunks * num_lines];
     check(unsafe {

@@ -31,6 +31,8 @@ where G::Scalar: Field + GpuName
         program: Program,
         maybe_abort: Option<&'a (dyn Fn() -> bool + Send + Sync)>,
     ) -> EcResult<Self> {
+        // the engine reads and writes `G::Curve` as [X, Y, Z] in place
+        ecgpu_ark::require_projective_xyz::<G>().map_err(EcError::Simple)?;
         Ok(SingleEcFftKernel { program, maybe_abort, _phantom: Default::default() })
     }
 
@@ -40,6 +42,7 @@ where G::Scalar: Field + GpuName
         &mut self, input: &mut [G::Curve], omega: &G::Scalar, log_n: u32,
     ) -> EcResult<()> {
         assert_eq!(input.len(), 1usize << log_n, "input length must be 2^log_n");
+        ecgpu_ark::require_projective_xyz::<G>().map_err(EcError::Simple)?;
         let curve = curve_id::<G>()?;
         require(&self.program, sys::ECG_KIND_EC_FFT, curve)?;
         let (cb, user) = abort_hook(&self.maybe_abort);
@@ -110,6 +113,7 @@ where
         for (input, &log_n) in inputs.iter().zip(log_ns) {
             assert_eq!(input.len(), 1usize << log_n, "input length must be 2^log_n");
         }
+        ecgpu_ark::require_projective_xyz::<G>().map_err(EcError::Simple)?;
         let curve = curve_id::<G>()?;
         for k in &self.kernels {
             require(&k.program, sys::ECG_KIND_EC_FFT, curve)?;

@@ -17,9 +17,9 @@ use std::os::raw::{c_int, c_void};
 use std::sync::{Arc, RwLock};
 
 use ag_types::{GpuCurveAffine, GpuName, GpuRepr, PrimeFieldRepr as PrimeField};
-use ark_ec::AffineRepr;
-use ark_ff::{One, Zero};
+use ark_ff::Zero;
 use ec_gpu_program::{EcError, EcResult};
+use ecgpu_ark::{ark_layout, ArkLayout};
 use ecgpu_sys as sys;
 use log::{error, info, warn};
 use rust_gpu_tools::{Device, Program};
@@ -27,54 +27,6 @@ use yastl::Scope;
 
 use super::{abort_hook, check, curve_id, require, MaybeAbort};
 use crate::threadpool::Worker;
-
-/// How the engine may touch `G` and `G::Curve` in place.  arkworks'
-/// short-Weierstrass `Affine { x, y, infinity: bool }` and `Projective
-/// { x, y, z }` carry no `repr(C)`, so their field order is probed once per
-/// kernel on the curve's generator instead of assumed (the reference reads
-/// `G::Curve` straight out of a device buffer, multiexp.rs:209-211):
-///   * `ark_affine`: x at offset 0, y right after it, the `infinity` flag in
-///     the byte after y, record size 2 coordinates + 8 -- the layout
-///     `ECG_BASES_ARK_AFFINE` reads on the device;
-///   * `projective_xyz`: `Projective::from(generator)` is the bytes of
-///     [x | y | one], i.e. the engine's Jacobian [X, Y, Z] result can be
-///     written in place.
-#[derive(Clone, Copy, Debug)]
-pub(crate) struct ArkLayout {
-    pub ark_affine: bool,
-    pub projective_xyz: bool,
-}
-
-fn bytes_of<T>(v: &T) -> &[u8] {
-    // only called on field elements and projective points: no padding bytes
-    unsafe { std::slice::from_raw_parts(v as *const T as *const u8, std::mem::size_of::<T>()) }
-}
-
-pub(crate) fn ark_layout<G: GpuCurveAffine>() -> ArkLayout {
-    let lq = std::mem::size_of::<<G as AffineRepr>::BaseField>();
-    let g = G::generator();
-    let (gx, gy) = match g.xy() {
-        Some(xy) => xy,
-        None => return ArkLayout { ark_affine: false, projective_xyz: false },
-    };
-    let at = |p: &G, f: &<G as AffineRepr>::BaseField| f as *const _ as usize - p as *const G as usize;
-    // the flag byte: the identity has it set, the generator clear (read only
-    // once x and y are known to fill the first 2 lq bytes)
-    let flag = |p: &G| unsafe { std::ptr::read((p as *const G as *const u8).add(2 * lq)) };
-    let ark_affine = std::mem::size_of::<G>() == 2 * lq + 8
-        && at(&g, gx) == 0
-        && at(&g, gy) == lq
-        && flag(&g) == 0
-        && flag(&G::zero()) == 1;
-    let p = g.into_group();
-    let one = <<G as AffineRepr>::BaseField as One>::one();
-    let pb = bytes_of(&p);
-    let projective_xyz = pb.len() == 3 * lq
-        && &pb[..lq] == bytes_of(gx)
-        && &pb[lq..2 * lq] == bytes_of(gy)
-        && &pb[2 * lq..] == bytes_of(&one);
-    ArkLayout { ark_affine, projective_xyz }
-}
 
 /// Multiexp on one device.
 pub struct SingleMultiexpKernel<'a, G>
@@ -129,8 +81,7 @@ where G: GpuCurveAffine + GpuName
         assert_eq!(bases.len(), exponents.len());
         require(&self.program, sys::ECG_KIND_MULTIEXP, self.curve)?;
         if !self.layout.projective_xyz {
-            return Err(EcError::Simple("arkworks Projective is not laid out as [x, y, z]; \
-                                        the engine's result cannot be written into G::Curve"));
+            return Err(EcError::Simple(ecgpu_ark::NOT_XYZ));
         }
         let words = std::mem::size_of::<G::Curve>() / 8;
         let mut out = vec![0u64; words];

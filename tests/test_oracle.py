@@ -155,6 +155,34 @@ def test_multiexp_cpu_rejects_identity_base():
 
 
 @pytest.mark.parametrize("cid", [0, 1])
+@pytest.mark.parametrize("n", [16, 64, 1000])
+def test_multiexp_cpu_bit255_windows(cid, n):
+    """multiexp_cpu's windows are (0..MODULUS_BIT_SIZE).step_by(c)
+    (multiexp_cpu.rs:320): it reads bits < ceil(bits/c)*c.  At n = 16 (c = 3)
+    and 64 (c = 5) that is <= 255 on both curves, so bit 255 of a BigInt is
+    dropped; at n = 1000 (c = 7) it is read.  The reference GPU kernel reads
+    all SCALAR_BITS = 256 (multiexp_backup.cl:42); the engine follows the GPU
+    kernel, and tests/test_gpu_msm.py compares on identical inputs only where
+    the two reference paths agree (n = 1000)."""
+    cv = po.CURVES[["bls12_381", "bn254"][cid]]
+    r = cv.fr.modulus
+    bits = 255 if cid == 0 else 254
+    c = 3 if n < 32 else int(np.ceil(np.log(n)))
+    reads_255 = -(-bits // c) * c > 255
+    assert reads_255 == (n == 1000)
+    a, b = 7, 11
+    B = co.gen_bases(cid, a, b, n, 4)
+    rng = np.random.default_rng(n + cid)
+    vals = [(1 << 255) | int.from_bytes(rng.bytes(32), "little") % (1 << 255) for _ in range(n)]
+    got = co.jac_to_affine(cid, co.multiexp_cpu(cid, B, co.u64arr(vals, 4), nthreads=4))
+    full = sum(s * (a + i * b) for i, s in enumerate(vals)) % r
+    low = sum((s - (1 << 255)) * (a + i * b) for i, s in enumerate(vals)) % r
+    want = full if reads_255 else low
+    assert (got == co.jac_to_affine(cid, co.gen_mul(cid, want))).all()
+    assert full != low
+
+
+@pytest.mark.parametrize("cid", [0, 1])
 def test_kat_construction(cid):
     """Bases P_i = (a + i b) G: sum s_i P_i == (sum s_i (a + i b) mod r) G."""
     cv = po.CURVES[["bls12_381", "bn254"][cid]]

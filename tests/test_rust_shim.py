@@ -270,7 +270,52 @@ def test_multiexp_reads_ark_affine_on_device_and_caches_arc_bases():
     assert "self.multiexp_cached(bases, exponents, false)" in _fn_body(src, "pub fn multiexp(\n        &self")
     # pinning follows the engine's cache keys
     assert "ecg_base_cache_keys" in src and "self.pinned.push(bases_arc.clone())" in src
-    assert "fn ark_layout<G: GpuCurveAffine>()" in src
+    assert "use ecgpu_ark::{ark_layout, ArkLayout};" in src and "let layout = ark_layout::<G>();" in src
+
+
+# engine calls whose output is Jacobian points the shims hand over as G::Curve
+POINT_WRITERS = ("ecg_ec_fft", "ecg_ec_fft_many", "ecg_multiple_multiexp", "ecg_msm", "ecg_msm_ex")
+
+
+def _fns(src):
+    """(name, body) of every `fn` in src (bodies by brace matching)."""
+    out = []
+    for m in re.finditer(r"\bfn\s+(\w+)\s*(<[^{;]*?>)?\s*\(", src):
+        i = src.find("{", m.end())
+        semi = src.find(";", m.end())
+        if i < 0 or (0 <= semi < i and "->" not in src[m.end():semi] and ")" in src[m.end():semi]):
+            continue
+        depth, j = 1, i + 1
+        while depth:
+            depth += {"{": 1, "}": -1}.get(src[j], 0)
+            j += 1
+        out.append((m.group(1), src[i:j]))
+    return out
+
+
+def test_no_shim_writes_curve_without_the_layout_probe():
+    """Every drop-in function that passes G::Curve memory to the engine (or
+    copies engine points into one) is guarded by the arkworks layout probe
+    (ecgpu-ark: require_projective_xyz, or the kernel's probed
+    layout.projective_xyz), and refuses the call when the probe fails
+    (VERDICT r04 weak 8)."""
+    probe = re.compile(r"require_projective_xyz::<\w+>\(\)|layout\.projective_xyz")
+    checked = []
+    for rel in ("ec-gpu-proxy/src/amd/multiexp.rs", "ec-gpu-proxy/src/amd/ec_fft.rs",
+                "ag-cuda-ec/src/multiexp.rs", "ag-cuda-ec/src/ec_fft.rs"):
+        src = open(os.path.join(RUST, rel)).read()
+        for name, body in _fns(src):
+            writes = [w for w in POINT_WRITERS if re.search(rf"sys::{w}\(", body)]
+            if writes:
+                assert probe.search(body), (rel, name, writes)
+                checked.append((rel, name))
+    assert len(checked) == 5, checked
+    lib = open(os.path.join(RUST, "ecgpu-ark/src/lib.rs")).read()
+    assert "pub fn ark_layout<A: AffineRepr>()" in lib and "pub fn require_projective_xyz" in lib
+    # the shared crate is a workspace member and a dependency of both drop-ins
+    assert '"ecgpu-ark"' in open(os.path.join(RUST, "Cargo.toml")).read()
+    assert "ecgpu-ark" in open(os.path.join(RUST, "ag-cuda-ec/Cargo.toml")).read()
+    assert '"ecgpu-ark"' in open(os.path.join(RUST, "ec-gpu-proxy/Cargo.amd.toml")).read()
 
 
 def test_ag_cuda_ec_upload_has_table_form_and_true_size():
