@@ -183,6 +183,9 @@ int comm_allgather(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t bytes,
 void comm_free(ecg_ctx* ctx) {
   if (ctx->comm) (void)ncclCommDestroy((ncclComm_t)ctx->comm);
   ctx->comm = nullptr;
+  if (ctx->comm_rec) (void)hipFree(ctx->comm_rec);
+  ctx->comm_rec = nullptr;
+  ctx->comm_rec_bytes = 0;
   ctx->xchg = nullptr;
   ctx->xchg_user = nullptr;
   ctx->comm_size = 1;
@@ -192,6 +195,43 @@ void comm_free(ecg_ctx* ctx) {
 // Status words ride in fixed-size records so ranks that disagree on the
 // call's arguments still exchange equal byte counts.
 constexpr int AGREE_WORDS = 4;
+// The largest status record: the MSM's [rc | curve | Jacobian partial].
+constexpr size_t REC_MAX_BYTES = (2 + 3 * (size_t)ECG_MAX_COORD_U64) * 8;
+
+// All-gather of one small host record per rank, for the status exchanges.
+// Nothing here allocates device memory: the host transport moves the host
+// records itself, and RCCL stages them through ctx->comm_rec, reserved at
+// ecg_comm_init.  So a rank whose call failed on a workspace allocation (or
+// anything else local) still joins the exchange and its peers learn of the
+// failure at once instead of waiting out the deadline.
+int comm_exchange_rec(ecg_ctx* ctx, const void* h_send, void* h_recv, size_t bytes, hipStream_t s,
+                      const char* what) {
+  ECG_TRY(need_comm(ctx, what));
+  const size_t P = (size_t)ctx->comm_size;
+  if (host_transport(ctx)) {
+    if (ctx->xchg(ECG_XCHG_ALLGATHER, h_send, h_recv, bytes, ctx->xchg_user) != 0) {
+      set_error("%s: the host transport failed", what);
+      return ECG_ERR_RCCL;
+    }
+    return ECG_OK;
+  }
+  if (!ctx->comm) {  // one rank, no communicator
+    memcpy(h_recv, h_send, bytes);
+    return ECG_OK;
+  }
+  if (bytes > REC_MAX_BYTES || !ctx->comm_rec || ctx->comm_rec_bytes < REC_MAX_BYTES + bytes * P) {
+    set_error("%s: status record of %zu bytes does not fit the reserved staging", what, bytes);
+    return ECG_ERR_INVALID;
+  }
+  uint8_t* d_rec = (uint8_t*)ctx->comm_rec;
+  uint8_t* d_all = d_rec + REC_MAX_BYTES;
+  ECG_HIP(hipMemcpyAsync(d_rec, h_send, bytes, hipMemcpyHostToDevice, s));
+  ECG_TRY(comm_allgather(ctx, d_rec, d_all, bytes, s));
+  ECG_TRY(comm_wait(ctx, s, what));
+  ECG_HIP(hipMemcpyAsync(h_recv, d_all, bytes * P, hipMemcpyDeviceToHost, s));
+  ECG_HIP(hipStreamSynchronize(s));
+  return ECG_OK;
+}
 
 int comm_agree(ecg_ctx* ctx, int local_rc, const uint64_t* agree, int n_agree, const char* what, hipStream_t s) {
   const int P = ctx->comm_size;
@@ -200,15 +240,9 @@ int comm_agree(ecg_ctx* ctx, int local_rc, const uint64_t* agree, int n_agree, c
   const std::string local_msg = local_rc != ECG_OK ? last_error_text() : "";
   uint64_t rec[1 + AGREE_WORDS] = {(uint64_t)(int64_t)local_rc, 0, 0, 0, 0};
   for (int i = 0; i < n_agree && i < AGREE_WORDS; i++) rec[1 + i] = agree[i];
-  void *d_rec, *d_all;
-  ECG_TRY(ws_get(ctx, "comm_agree", sizeof rec, &d_rec));
-  ECG_TRY(ws_get(ctx, "comm_agree_all", sizeof rec * P, &d_all));
+  if (local_rc != ECG_OK) (void)hipStreamSynchronize(s);  // the failed step's work is done or abandoned
   std::vector<uint64_t> all((1 + AGREE_WORDS) * (size_t)P);
-  ECG_HIP(hipMemcpyAsync(d_rec, rec, sizeof rec, hipMemcpyHostToDevice, s));
-  ECG_TRY(comm_allgather(ctx, d_rec, d_all, sizeof rec, s));
-  ECG_TRY(comm_wait(ctx, s, what));
-  ECG_HIP(hipMemcpyAsync(all.data(), d_all, sizeof rec * P, hipMemcpyDeviceToHost, s));
-  ECG_HIP(hipStreamSynchronize(s));
+  ECG_TRY(comm_exchange_rec(ctx, rec, all.data(), sizeof rec, s, what));
   for (int r = 0; r < P; r++) {
     const int rc = (int)(int64_t)all[(size_t)r * (1 + AGREE_WORDS)];
     if (rc == ECG_OK) continue;
@@ -263,26 +297,37 @@ int ecg_comm_init(ecg_ctx* ctx, int nranks, int rank, const uint8_t* unique_id) 
   (void)hipStreamSynchronize(ctx->stream);
   comm_free(ctx);  // back to the single-rank state until the new communicator exists
   if (!unique_id) return ECG_OK;  // one rank, no communicator
+  // the status-record staging (comm_exchange_rec), before any collective:
+  // a rank that cannot allocate it never enters the communicator's init
+  {
+    const size_t bytes = REC_MAX_BYTES * ((size_t)nranks + 1);
+    hipError_t e = hipMalloc(&ctx->comm_rec, bytes);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      ctx->comm_rec = nullptr;
+      set_error("ecg_comm_init: staging of %zu bytes for the status records failed: %s", bytes, hipGetErrorString(e));
+      return ECG_ERR_NOMEM;
+    }
+    ctx->comm_rec_bytes = bytes;
+  }
   ncclUniqueId id;
   memcpy(id.internal, unique_id, NCCL_UNIQUE_ID_BYTES);
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
   cfg.blocking = 0;  // every wait below runs under the deadline
   ncclComm_t c = nullptr;
   ncclResult_t r = ncclCommInitRankConfig(&c, nranks, id, rank, &cfg);
+  // from here on the context is an nranks-rank context: if the communicator
+  // fails to come up, comm stays null and need_comm refuses every
+  // distributed call until ecg_comm_init runs again (not a silent 1-rank run)
+  ctx->comm_size = nranks;
+  ctx->comm_rank = rank;
   if (r != ncclSuccess && r != ncclInProgress) {
     set_error("ncclCommInitRankConfig: %s", ncclGetErrorString(r));
     if (c) (void)ncclCommAbort(c);
     return ECG_ERR_RCCL;
   }
   ctx->comm = c;
-  ctx->comm_size = nranks;
-  ctx->comm_rank = rank;
-  int rc = rccl_settle(ctx, r, "ecg_comm_init");
-  if (rc != ECG_OK) {
-    ctx->comm_size = 1;  // nothing to refuse: the caller re-initialises
-    ctx->comm_rank = 0;
-  }
-  return rc;
+  return rccl_settle(ctx, r, "ecg_comm_init");
 }
 
 int ecg_comm_init_host(ecg_ctx* ctx, int nranks, int rank, ecg_xchg_cb xchg, void* user) {
@@ -297,6 +342,40 @@ int ecg_comm_init_host(ecg_ctx* ctx, int nranks, int rank, ecg_xchg_cb xchg, voi
   ctx->xchg_user = user;
   ctx->comm_size = nranks;
   ctx->comm_rank = rank;
+  return ECG_OK;
+}
+
+int ecg_comm_info(ecg_ctx* ctx, int* nranks, int* rank, int* device, char* bus_id, size_t bus_cap, int* transport) {
+  ECG_ENTER(ctx);
+  int n = ctx->comm_size, r = ctx->comm_rank, d = ctx->device;
+  int t = host_transport(ctx) ? ECG_COMM_HOST : ctx->comm ? ECG_COMM_RCCL : ctx->comm_size > 1 ? ECG_COMM_FAILED
+                                                                                                 : ECG_COMM_NONE;
+  if (t == ECG_COMM_RCCL) {  // what the communicator itself reports
+    ncclComm_t c = (ncclComm_t)ctx->comm;
+    if (ncclCommCount(c, &n) != ncclSuccess || ncclCommUserRank(c, &r) != ncclSuccess ||
+        ncclCommCuDevice(c, &d) != ncclSuccess) {
+      set_error("ecg_comm_info: the RCCL communicator did not answer its queries");
+      return ECG_ERR_RCCL;
+    }
+  }
+  if (nranks) *nranks = n;
+  if (rank) *rank = r;
+  if (device) *device = d;
+  if (transport) *transport = t;
+  if (bus_id && bus_cap) {
+    bus_id[0] = 0;
+    ECG_HIP(hipDeviceGetPCIBusId(bus_id, (int)bus_cap, d));
+  }
+  return ECG_OK;
+}
+
+int ecg_comm_last_exchange(ecg_ctx* ctx, double* us) {
+  ECG_ENTER(ctx);
+  if (!us) {
+    set_error("ecg_comm_last_exchange: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  *us = ctx->comm_last_xchg_us;
   return ECG_OK;
 }
 
@@ -351,15 +430,14 @@ int ecg_msm_dist_ex(ecg_ctx* ctx, int curve_id, const void* d_bases, const void*
   rec[0] = (uint64_t)(int64_t)rc;
   rec[1] = (uint64_t)(uint32_t)curve_id;
   const int P = ctx->comm_size;
-  void *d_rec, *d_all;
-  ECG_TRY(ws_get(ctx, "dist_rec", sizeof rec, &d_rec));
-  ECG_TRY(ws_get(ctx, "dist_all", sizeof rec * P, &d_all));
-  ECG_HIP(hipMemcpyAsync(d_rec, rec, sizeof rec, hipMemcpyHostToDevice, s));
-  ECG_TRY(comm_allgather(ctx, d_rec, d_all, sizeof rec, s));
-  ECG_TRY(comm_wait(ctx, s, "ecg_msm_dist"));
+  static_assert(sizeof rec <= REC_MAX_BYTES, "MSM status record exceeds the reserved staging");
+  // one exchange, no allocation on this path: every rank joins it whatever
+  // its local step did (comm_exchange_rec)
   std::vector<uint64_t> all((2 + PW) * (size_t)P);
-  ECG_HIP(hipMemcpyAsync(all.data(), d_all, sizeof rec * P, hipMemcpyDeviceToHost, s));
-  ECG_HIP(hipStreamSynchronize(s));
+  const auto t_x = std::chrono::steady_clock::now();
+  ECG_TRY(comm_exchange_rec(ctx, rec, all.data(), sizeof rec, s, "ecg_msm_dist"));
+  ctx->comm_last_xchg_us =
+      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_x).count();
   for (int r = 0; r < P; r++) {  // the lowest failing rank's code, on every rank
     const int rrc = (int)(int64_t)all[(size_t)r * (2 + PW)];
     if (rrc == ECG_OK) continue;

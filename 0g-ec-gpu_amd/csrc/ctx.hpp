@@ -98,6 +98,15 @@ struct ecg_ctx {
   ecg_xchg_cb xchg = nullptr;
   void* xchg_user = nullptr;
   uint32_t comm_timeout_ms = 0;  // 0 = ECG_COMM_TIMEOUT_S or the default
+  // device staging of the status records (comm.cpp comm_exchange_rec),
+  // reserved when an RCCL communicator is set up so that a rank whose call
+  // failed on an allocation still joins the status exchange
+  void* comm_rec = nullptr;
+  size_t comm_rec_bytes = 0;
+  // wall time of the last distributed MSM's status + partial exchange
+  double comm_last_xchg_us = 0.0;
+  // workspace cap (ecg_ctx_set_mem_limit; 0 = the device's memory)
+  size_t mem_limit = 0;
   // kernel timing (HIP events on the launch stream)
   std::map<std::string, ecg::KernelTimes> ktimes;
   std::vector<hipEvent_t> event_pool;
@@ -107,6 +116,11 @@ namespace ecg {
 
 // Make ctx's device current for this host thread.
 int ctx_enter(ecg_ctx* ctx);
+// Device memory this context plans with: the device's, or its
+// ecg_ctx_set_mem_limit cap when that is lower.
+inline size_t ctx_mem(const ecg_ctx* ctx) {
+  return ctx->mem_limit && ctx->mem_limit < ctx->mem_bytes ? ctx->mem_limit : ctx->mem_bytes;
+}
 // Grow-only named device buffer.
 int ws_get(ecg_ctx* ctx, const char* name, size_t bytes, void** out);
 void ws_release(ecg_ctx* ctx, const char* name);

@@ -48,6 +48,16 @@ int ctx_enter(ecg_ctx* ctx) {
 int ws_get(ecg_ctx* ctx, const char* name, size_t bytes, void** out) {
   auto& b = ctx->ws[name];
   if (bytes == 0) bytes = 16;
+  if (b.bytes < bytes && ctx->mem_limit) {  // ecg_ctx_set_mem_limit
+    size_t total = bytes;
+    for (const auto& kv : ctx->ws)
+      if (&kv.second != &b) total += kv.second.bytes;
+    if (total > ctx->mem_limit) {
+      set_error("device allocation of %zu bytes for '%s' refused: the context's workspace would reach %zu bytes, "
+                "over its limit of %zu (ecg_ctx_set_mem_limit)", bytes, name, total, ctx->mem_limit);
+      return ECG_ERR_NOMEM;
+    }
+  }
   if (b.bytes < bytes) {
     if (b.ptr) {
       // the buffer may still be in use by queued work
@@ -228,7 +238,7 @@ int ecg_ctx_info(ecg_ctx* ctx, size_t* mem_bytes, int* compute_units) {
     set_error("null context");
     return ECG_ERR_INVALID;
   }
-  if (mem_bytes) *mem_bytes = ctx->mem_bytes;
+  if (mem_bytes) *mem_bytes = ctx_mem(ctx);
   if (compute_units) *compute_units = ctx->compute_units;
   return ECG_OK;
 }
@@ -943,6 +953,12 @@ int ecg_gen_bases_dev(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint6
     return ECG_ERR_INVALID;
   }
   return gen_bases_run(ctx, curve_id, a, b, n, d_out, pick_stream(ctx, stream));
+}
+
+int ecg_ctx_set_mem_limit(ecg_ctx* ctx, size_t bytes) {
+  ECG_ENTER(ctx);
+  ctx->mem_limit = bytes;
+  return ECG_OK;
 }
 
 int ecg_ctx_set_msm_chunk(ecg_ctx* ctx, size_t max_terms) {

@@ -68,8 +68,17 @@ static uint32_t env_u32(const char* name, uint32_t dflt) {
   const char* e = getenv(name);
   return e ? (uint32_t)strtoul(e, nullptr, 10) : dflt;
 }
+// An A/B knob that must lie in [lo, hi]: anything else (unset, garbage, out
+// of range) keeps the default.
+static uint32_t env_u32_in(const char* name, uint32_t dflt, uint32_t lo, uint32_t hi) {
+  const char* e = getenv(name);
+  if (!e || !*e) return dflt;
+  char* end = nullptr;
+  const unsigned long v = strtoul(e, &end, 10);
+  return (*end == 0 && v >= lo && v <= hi) ? (uint32_t)v : dflt;
+}
 static uint32_t msm_red_seg() {  // buckets per reduction segment (0: plan_reduction picks)
-  static uint32_t v = env_u32("ECG_MSM_RED_SEG", 0);
+  static uint32_t v = env_u32_in("ECG_MSM_RED_SEG", 0, 1, 1u << 16);
   return v;
 }
 // Records per thread in msm_combine: each level is a serial chain of that many
@@ -87,7 +96,7 @@ static bool msm_short_runs() {  // A/B switch: ECG_MSM_SHORT=0 sends every recor
   return v;
 }
 static uint32_t msm_acc_seg() {  // sorted entries per accumulation thread
-  static uint32_t v = env_u32("ECG_MSM_ACC_SEG", 128);
+  static uint32_t v = env_u32_in("ECG_MSM_ACC_SEG", 128, 16, 4096);
   return v;
 }
 
@@ -105,7 +114,7 @@ static bool msm_pw_one_enabled() {  // A/B switch: ECG_MSM_PW1=0 sorts every blo
   return v;
 }
 static int msm_sort_cfg() {  // onesweep config of the per-block sorts (A/B: ECG_MSM_SORTCFG)
-  static const int v = (int)env_u32("ECG_MSM_SORTCFG", 2);
+  static const int v = (int)env_u32_in("ECG_MSM_SORTCFG", 2, 0, 3);
   return v;
 }
 
@@ -201,7 +210,7 @@ static void plan_reduction(MsmPlan& pl, uint32_t waves = 2) {
 // below) per task (bucket accumulation vs reduction vs window-fold adds; a
 // reduction step is ~2 full adds, ~1.4x a mixed add).  nbits = scalar MODULUS_BIT_SIZE.  forced_c != 0 pins c.
 static MsmPlan make_plan(size_t n, uint32_t nbits, uint32_t forced_c = 0) {
-  if (!forced_c) forced_c = env_u32("ECG_MSM_C", 0);  // A/B: pin the single-MSM window
+  if (!forced_c) forced_c = env_u32_in("ECG_MSM_C", 0, 2, 22);  // A/B: pin the single-MSM window
   double best = 1e300;
   MsmPlan pl{};
   for (uint32_t c = 1; c <= 22; c++) {
@@ -560,7 +569,7 @@ constexpr uint32_t MSM_SHORT_RUN = 16;
 constexpr uint32_t MSM_SHORT_SEG = 4;
 constexpr size_t MSM_SHORT_MAX_RECS_DEFAULT_LOG = 21;
 static size_t msm_short_max_recs() {  // A/B: ECG_MSM_SHORT_LOG
-  static const size_t v = (size_t)1 << env_u32("ECG_MSM_SHORT_LOG", MSM_SHORT_MAX_RECS_DEFAULT_LOG);
+  static const size_t v = (size_t)1 << env_u32_in("ECG_MSM_SHORT_LOG", MSM_SHORT_MAX_RECS_DEFAULT_LOG, 4, 31);
   return v;
 }
 template <class F>
@@ -873,7 +882,7 @@ static uint32_t offset_bits(uint32_t S) {  // KB of msm_offset_bits_kernel
 // over K = 8; 2^26 (KB = 13) K = 32 within noise of 16
 // (profiles/r04/tail_ls_k_ab.txt).  ECG_MSM_BITS_K pins K.
 static uint32_t offset_bits_k(uint32_t S) {
-  const uint32_t pinned = env_u32("ECG_MSM_BITS_K", 0);
+  const uint32_t pinned = env_u32_in("ECG_MSM_BITS_K", 0, 1, 64);
   if (pinned) return pinned;
   const uint32_t kb = offset_bits(S);
   const uint32_t k = kb > 8 ? 1u << (kb - 8) : 2u;
@@ -972,7 +981,7 @@ __global__ void __launch_bounds__(64)
   if ((g & ((1u << PB) - 1)) == 0) store_xyzz(&out[t], acc);
 }
 static uint32_t msm_fold_lanes() {  // A/B: ECG_MSM_FOLD_PAIRS = 0 / 1 (one lane per task), 2 (pairs), 4 (quads)
-  static const uint32_t v = env_u32("ECG_MSM_FOLD_PAIRS", 4);
+  static const uint32_t v = env_u32_in("ECG_MSM_FOLD_PAIRS", 4, 0, 4);
   return v;
 }
 
@@ -1661,19 +1670,30 @@ void msm_host_fold_bits(const XYZZ<typename C::Fq>* sums, const MsmPlan& e, host
 // the sort's scratch.  MEMORY_PADDING of the device memory and the resident
 // base cache are left alone.  ecg_ctx_set_msm_chunk pins the value instead.
 template <class C>
-size_t msm_pass_terms(const ecg_ctx* ctx) {
-  if (ctx->msm_chunk) return ctx->msm_chunk;
+double msm_term_bytes(const MsmPlan& pl) {
   using F = typename C::Fq;
   constexpr bool rr = MsmField<C>::rr;
   using AF = typename MsmField<C>::type;
-  const MsmPlan pl = make_plan((size_t)1 << 26, (uint32_t)C::FrParams::BITS);
-  const double per_term = 2.0 * sizeof(F) + 32.0 + (rr ? (double)BaseLayout<AF>::BYTES : 0.0) + 16.0 * pl.W +
-                          2.0 * pl.W / pl.seg * (sizeof(XYZZ<AF>) + 4) * (1.0 + 1.0 / 16);
-  const double fixed = (double)pl.W * pl.B * sizeof(XYZZ<AF>) + 256.0 * (1 << 20);
+  return 2.0 * sizeof(F) + 32.0 + (rr ? (double)BaseLayout<AF>::BYTES : 0.0) + 16.0 * pl.W +
+         2.0 * pl.W / pl.seg * (sizeof(XYZZ<AF>) + 4) * (1.0 + 1.0 / 16);
+}
+
+// Device memory left for an MSM's workspace: (1 - MEMORY_PADDING) of the
+// context's memory, minus the resident base cache and 256 MB of scratch.
+template <class C>
+double msm_mem_budget(const ecg_ctx* ctx) {
   double cached = 0;
   for (const auto& e : ctx->base_cache) cached += (double)e.n * msm_base_record_bytes<C>();  // prepared entries
-  const double budget = (double)ctx->mem_bytes * (1.0 - MSM_MEMORY_PADDING) - cached - fixed;
-  double t = budget / per_term;
+  return (double)ctx_mem(ctx) * (1.0 - MSM_MEMORY_PADDING) - cached - 256.0 * (1 << 20);
+}
+
+template <class C>
+size_t msm_pass_terms(const ecg_ctx* ctx) {
+  if (ctx->msm_chunk) return ctx->msm_chunk;
+  using AF = typename MsmField<C>::type;
+  const MsmPlan pl = make_plan((size_t)1 << 26, (uint32_t)C::FrParams::BITS);
+  const double fixed = (double)pl.W * pl.B * sizeof(XYZZ<AF>);  // one bucket array
+  double t = (msm_mem_budget<C>(ctx) - fixed) / msm_term_bytes<C>(pl);
   if (!(t >= (double)(1u << 16))) t = (double)(1u << 16);  // tiny / unknown memory: still make progress
   if (t > (double)0x7fffffffu) t = (double)0x7fffffffu;   // 31-bit term indices
   return (size_t)t;
@@ -1718,7 +1738,7 @@ int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_
 
 
 static uint32_t msm_h2d_passes() {  // host-slice pipeline depth (A/B: ECG_MSM_H2D_PASSES)
-  static const uint32_t v = env_u32("ECG_MSM_H2D_PASSES", 4);
+  static const uint32_t v = env_u32_in("ECG_MSM_H2D_PASSES", 4, 1, 64);
   return v ? v : 1;
 }
 
@@ -1739,6 +1759,20 @@ static uint32_t msm_h2d_passes() {  // host-slice pipeline depth (A/B: ECG_MSM_H
 // the passes grow geometrically (first n / 16, then x2): the first pass's
 // upload is the only one not hidden behind compute.
 constexpr uint32_t MSM_MAX_SLOTS = 8;
+// Bucket slots a pipelined MSM may hold at once: one bucket array per pass of
+// a batch (W x B XYZZ buckets each; 1.5 GB for BLS12-381 at c = 20, 5.6 GB at
+// c = 22), as many as the memory left after the largest pass's per-term
+// workspace allows, at most MSM_MAX_SLOTS.  Passes beyond it form more batches
+// (one reduction each).  msm_pass_terms budgets one array only.
+template <class C>
+uint32_t msm_slot_cap(const ecg_ctx* ctx, const MsmPlan& pl, size_t pmax) {
+  using AF = typename MsmField<C>::type;
+  const double slot = (double)pl.G * pl.B * sizeof(XYZZ<AF>);
+  const double left = msm_mem_budget<C>(ctx) - (double)pmax * msm_term_bytes<C>(pl);
+  const double k = left / slot;
+  if (!(k >= 1.0)) return 1;
+  return k >= MSM_MAX_SLOTS ? MSM_MAX_SLOTS : (uint32_t)k;
+}
 // fill (a cache miss of ecg_msm_ex, msm_prepared_alloc'd `bases`): the host
 // bases of each pass go up with its scalars (104 B ark records or 96 B [x, y])
 // and become the buffer's records on the device before the pass reads them;
@@ -1769,8 +1803,8 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
     poff.push_back(n);
   } else if (n >= ((size_t)1 << 22) && resident && !fill) {
     // A/B: ECG_MSM_PASS_FIRST (1/x of n) and ECG_MSM_PASS_GROWTH
-    static const uint32_t first_div = std::max(1u, env_u32("ECG_MSM_PASS_FIRST", 16));
-    static const uint32_t growth = std::max(2u, env_u32("ECG_MSM_PASS_GROWTH", 3));
+    static const uint32_t first_div = env_u32_in("ECG_MSM_PASS_FIRST", 16, 1, 1024);
+    static const uint32_t growth = env_u32_in("ECG_MSM_PASS_GROWTH", 3, 2, 16);
     size_t m = std::max<size_t>((n / first_div + 255) / 256 * 256, 1);
     while (poff.back() < n) {
       const size_t left = n - poff.back();
@@ -1791,8 +1825,9 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
   const MsmPlan pl = bf.tab_c ? make_tab_plan(1, (uint32_t)C::FrParams::BITS, bf.tab_c, bf.tab_n)
                               : make_plan(n, (uint32_t)C::FrParams::BITS);
   const size_t nsums = msm_single_sums(msm_eff_plan<C>(pl));
-  const size_t nbatch = (np + MSM_MAX_SLOTS - 1) / MSM_MAX_SLOTS;
-  const uint32_t slots = (uint32_t)std::min<size_t>(np, MSM_MAX_SLOTS);
+  const uint32_t slot_cap = msm_slot_cap<C>(ctx, pl, pmax);
+  const size_t nbatch = (np + slot_cap - 1) / slot_cap;
+  const uint32_t slots = (uint32_t)std::min<size_t>(np, slot_cap);
   // bytes per base of the resident buffer (all of its table rows)
   const size_t rstride = msm_base_record_bytes<C>() * (bf.tab_c ? msm_table_windows<C>(bf.tab_c) : 1u);
   void *ib[2] = {nullptr, nullptr}, *is[2] = {nullptr, nullptr}, *sums, *fxy = nullptr;
@@ -1834,9 +1869,9 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
     const int b = (int)(k & 1);
     const size_t m = poff[k + 1] - poff[k];
     const MsmGeom g{1, 1, m, m, scalar_mont};
-    const size_t batch = k / MSM_MAX_SLOTS;
-    const uint32_t slot = (uint32_t)(k % MSM_MAX_SLOTS);
-    const bool last_of_batch = slot + 1 == MSM_MAX_SLOTS || k + 1 == np;
+    const size_t batch = k / slot_cap;
+    const uint32_t slot = (uint32_t)(k % slot_cap);
+    const bool last_of_batch = slot + 1 == slot_cap || k + 1 == np;
     const void* bp = resident ? (const void*)((const uint8_t*)bases + poff[k] * rstride) : ib[b];
     rc = [&]() -> int {
       ECG_HIP(hipStreamWaitEvent(cs, up[b], 0));

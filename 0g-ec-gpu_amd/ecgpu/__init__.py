@@ -119,6 +119,11 @@ _SIGS = {
     "ecg_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
     "ecg_msm_chunk_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "ecg_ctx_set_msm_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "ecg_ctx_set_mem_limit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "ecg_comm_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                     ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_size_t,
+                                     ctypes.POINTER(ctypes.c_int)]),
+    "ecg_comm_last_exchange": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "ecg_runtime_info": (ctypes.c_char_p, []),
     "ecg_msm_table_window": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_size_t]),
     "ecg_comm_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
@@ -350,6 +355,11 @@ class Program:
     def set_msm_chunk(self, max_terms: int) -> None:
         """Pin the terms per MSM device pass (0 = derived from device memory)."""
         _check(lib().ecg_ctx_set_msm_chunk(self.handle, int(max_terms)), "set_msm_chunk")
+
+    def set_mem_limit(self, nbytes: int) -> None:
+        """Cap the memory this context plans with and allocates as scratch
+        (ecg_ctx_set_mem_limit; 0 = the device's memory)."""
+        _check(lib().ecg_ctx_set_mem_limit(self.handle, int(nbytes)), "set_mem_limit")
 
     def kernel_time(self, name: str) -> tuple[float, int]:
         ms = ctypes.c_double()

@@ -406,6 +406,48 @@ def comm_init_host(prog, rank: int, world: int, exchange: Callable[[int, bytes, 
     ecgpu._check(L.ecg_comm_init_host(prog.handle, world, rank, c_cb, None), "comm_init_host")
 
 
+TRANSPORTS = {0: "none", 1: "rccl", 2: "host", 3: "failed"}
+
+
+def comm_info(prog) -> dict:
+    """What this rank's communicator reports (ecg_comm_info): for RCCL the
+    communicator's own ncclCommCount / ncclCommUserRank / ncclCommCuDevice,
+    and the PCI bus id of that device."""
+    import ctypes
+
+    import ecgpu
+
+    n, r, d, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    bus = ctypes.create_string_buffer(64)
+    ecgpu._check(ecgpu.lib().ecg_comm_info(prog.handle, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d), bus,
+                                           len(bus), ctypes.byref(t)), "comm_info")
+    return {"count": n.value, "rank": r.value, "device": d.value, "pci_bus_id": bus.value.decode(),
+            "transport": TRANSPORTS.get(t.value, str(t.value))}
+
+
+def last_exchange_us(prog) -> float:
+    """Wall time of the last msm_dist's status + partial exchange (us)."""
+    import ctypes
+
+    import ecgpu
+
+    us = ctypes.c_double()
+    ecgpu._check(ecgpu.lib().ecg_comm_last_exchange(prog.handle, ctypes.byref(us)), "comm_last_exchange")
+    return us.value
+
+
+def comm_record(infos: list) -> dict:
+    """rank 0's summary of every rank's comm_info (bench.py's `rccl` field):
+    the rank count the communicators hold, their ranks in order, their
+    devices by PCI bus id, and whether those devices are distinct."""
+    buses = [i["pci_bus_id"] for i in infos]
+    return {"transport": sorted({i["transport"] for i in infos}),
+            "count": sorted({i["count"] for i in infos}),
+            "ranks": [i["rank"] for i in infos],
+            "devices": buses,
+            "distinct": len(set(buses)) == len(buses)}
+
+
 class LocalExchange:
     """In-process host transport for `world` ranks driven by threads (one
     context each, e.g. all on one GPU): exchange_for(rank) is the rank's

@@ -62,7 +62,10 @@ KAT_B = 0x0FEDCBA987654321
 # the tight-slack layout bn254_fq9_rr)
 RR_LIMBS = {0: 14, 1: 9}
 RR_BITS = {0: 29, 1: 29}
-FR_RR_MADS = 2 * 9 * 9         # v_mad_u64_u32 per reduced-radix Fr product (9 x 29-bit limbs, ntt.hip)
+# v_mad_u64_u32 per reduced-radix Fr product as ntt.hip executes it (9 x 29-bit limbs: 81 schoolbook +
+# 81 reduction mads; BLS12-381's r = 1 mod 2^32 drops the m*P[0] mad of each of the 9 reduction columns
+# in the ceil-carry form, fieldrr.hpp rr_ceil_carry)
+FR_RR_MADS = {0: 2 * 9 * 9 - 9, 1: 2 * 9 * 9}
 
 
 def madd_mads(nl: int) -> int:
@@ -224,6 +227,9 @@ def main():
         edist.comm_init_host(prog, rank, world, edist.hostgroup_exchange(group))
     elif world > 1:
         edist.comm_init(prog, rank, world, group.broadcast)
+    # what each rank's communicator itself reports (ranks, device PCI ids): rank 0's
+    # record proves an N > 1 line ran N ranks on N distinct devices
+    comm = edist.comm_record(group.allgather(edist.comm_info(prog))) if world > 1 else None
     nthreads = cpu_threads(args.cpu_threads)
 
     # ------------------------------------------------------------ MSM inputs (HBM-resident)
@@ -278,6 +284,8 @@ def main():
     barrier()
     msm_s = group.max(time.perf_counter() - t0) / args.steps
     acc_avg_ms = group.max(acc_ms / max(acc_launch, 1))
+    if comm is not None:  # the last step's status + partial all-gather, slowest rank
+        comm["msm_allgather_us"] = group.max(edist.last_exchange_us(prog))
     msm_result = result.copy()
     # the same MSM over the [x, y] bases, converting them inside the step (reported, not `value`)
     unprep_ms = None
@@ -680,6 +688,7 @@ def main():
                              "traffic_unit": "GB/launch", "traffic_source": ntt_src, "kernel": "ntt_pass",
                              "avg_ms": pass_avg_ms, "note": "HBM fraction of a VALU-bound pass (64 B/element)"}},
         "ntt_dist": ntt_dist,
+        "rccl": comm,
         "checks": checks,
         "cpu_baseline": cpu_baseline,
         "e2e_api": e2e,
@@ -688,10 +697,10 @@ def main():
     }
     muls = ntt_fr_muls(log_n)
     # reduced-radix Fr product (fieldrr.hpp, 9 x 29-bit limbs): 81 schoolbook + 81 reduction mads
-    mad_rate = muls * FR_RR_MADS / (pass_ms / args.steps / 1e3) / 1e12
+    mad_rate = muls * FR_RR_MADS[cid] / (pass_ms / args.steps / 1e3) / 1e12
     line["ntt"]["valu"] = {"kernel": "ntt_pass", "achieved": mad_rate, "peak": MAD_PEAK_T,
                            "unit": "T v_mad_u64_u32/s", "frac": mad_rate / MAD_PEAK_T,
-                           "note": f"{muls / n_ntt:.2f} Fr products per element per transform x {FR_RR_MADS} "
+                           "note": f"{muls / n_ntt:.2f} Fr products per element per transform x {FR_RR_MADS[cid]} "
                                    "v_mad_u64_u32 / kernel time; peak as the MSM roofline's"}
     print(json.dumps(line))
     group.barrier()

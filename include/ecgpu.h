@@ -83,6 +83,12 @@ int ecg_ctx_synchronize(ecg_ctx *ctx);
  * ecg_ctx_set_msm_chunk pins it (1 .. 2^31-1; 0 restores the derived value). */
 int ecg_msm_chunk_size(ecg_ctx *ctx, int curve_id, size_t *out_terms);
 int ecg_ctx_set_msm_chunk(ecg_ctx *ctx, size_t max_terms);
+/* Cap the device memory this context plans with and allocates as scratch
+ * (bytes; 0 = the device's memory): calc_chunk_size's pass sizing uses it,
+ * and a scratch allocation that would take the context's workspace past it
+ * fails with ECG_ERR_NOMEM.  For ranks or provers that share one GPU, as the
+ * reference's MEMORY_PADDING leaves room for other users (multiexp.rs:24). */
+int ecg_ctx_set_mem_limit(ecg_ctx *ctx, size_t bytes);
 /* "hip=<version> (<libamdhip64 path>); rccl=<version> (<librccl path>)": the
  * HIP runtime and RCCL this process actually bound (launchers check it is the
  * ROCm install's, not another copy loaded earlier into the process). */
@@ -323,9 +329,24 @@ int ecg_msm_check_bases(int curve_id, const uint64_t *bases_xy, const uint64_t *
  * non-blocking: initialisation and every collective wait under a deadline
  * (ecg_comm_set_timeout; default ECG_COMM_TIMEOUT_S or 300 s), after which
  * the communicator is aborted and the call returns ECG_ERR_RCCL (a peer that
- * crashed or never arrived).  An aborted communicator refuses later
- * distributed calls until ecg_comm_init runs again. */
+ * crashed or never arrived).  An aborted communicator, or one whose
+ * ecg_comm_init failed, refuses later distributed calls until ecg_comm_init
+ * runs again.  The status records travel through staging reserved at
+ * ecg_comm_init, so no allocation can keep a failed rank out of the status
+ * exchange. */
 int ecg_comm_unique_id(uint8_t *out /* 128 bytes */);
+/* What the context's communicator reports: rank count, this rank and its HIP
+ * device (ncclCommCount / ncclCommUserRank / ncclCommCuDevice for RCCL; the
+ * init arguments for the host transport), the device's PCI bus id
+ * (NUL-terminated, bus_cap bytes, may be NULL) and the transport. */
+#define ECG_COMM_NONE 0   /* one rank, no communicator */
+#define ECG_COMM_RCCL 1
+#define ECG_COMM_HOST 2
+#define ECG_COMM_FAILED 3 /* several ranks, communicator aborted or never up */
+int ecg_comm_info(ecg_ctx *ctx, int *nranks, int *rank, int *device, char *bus_id, size_t bus_cap,
+                  int *transport);
+/* Wall time (us) of the last ecg_msm_dist's status + partial exchange. */
+int ecg_comm_last_exchange(ecg_ctx *ctx, double *us);
 int ecg_comm_init(ecg_ctx *ctx, int nranks, int rank, const uint8_t *unique_id);
 void ecg_comm_destroy(ecg_ctx *ctx);
 /* Deadline of communicator initialisation and of each exchange, in ms

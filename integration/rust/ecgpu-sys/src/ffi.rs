@@ -53,6 +53,11 @@ pub type ecg_abort_cb = Option<unsafe extern "C" fn(user: *mut c_void) -> c_int>
 // ---- host transport ops (ecg_comm_init_host) -----------------------------------
 pub const ECG_XCHG_ALLGATHER: c_int = 0;
 pub const ECG_XCHG_ALLTOALL: c_int = 1;
+// ecg_comm_info transports
+pub const ECG_COMM_NONE: c_int = 0;
+pub const ECG_COMM_RCCL: c_int = 1;
+pub const ECG_COMM_HOST: c_int = 2;
+pub const ECG_COMM_FAILED: c_int = 3;
 
 /// `typedef int (*ecg_xchg_cb)(int op, const void *send, void *recv, size_t
 /// bytes, void *user)`: the launcher's group moves the exchange bytes
@@ -77,6 +82,7 @@ extern "C" {
     pub fn ecg_ctx_synchronize(ctx: *mut ecg_ctx) -> c_int;
     pub fn ecg_msm_chunk_size(ctx: *mut ecg_ctx, curve_id: c_int, out_terms: *mut usize) -> c_int;
     pub fn ecg_ctx_set_msm_chunk(ctx: *mut ecg_ctx, max_terms: usize) -> c_int;
+    pub fn ecg_ctx_set_mem_limit(ctx: *mut ecg_ctx, bytes: usize) -> c_int;
     pub fn ecg_runtime_info() -> *const c_char;
     pub fn ecg_last_error() -> *const c_char;
     pub fn ecg_version() -> *const c_char;
@@ -147,6 +153,9 @@ extern "C" {
     pub fn ecg_comm_init(ctx: *mut ecg_ctx, nranks: c_int, rank: c_int, unique_id: *const u8) -> c_int;
     pub fn ecg_comm_destroy(ctx: *mut ecg_ctx);
     pub fn ecg_comm_set_timeout(ctx: *mut ecg_ctx, ms: u32) -> c_int;
+    pub fn ecg_comm_info(ctx: *mut ecg_ctx, nranks: *mut c_int, rank: *mut c_int, device: *mut c_int,
+                         bus_id: *mut c_char, bus_cap: usize, transport: *mut c_int) -> c_int;
+    pub fn ecg_comm_last_exchange(ctx: *mut ecg_ctx, us: *mut f64) -> c_int;
     pub fn ecg_comm_init_host(ctx: *mut ecg_ctx, nranks: c_int, rank: c_int, xchg: ecg_xchg_cb,
                               user: *mut c_void) -> c_int;
     pub fn ecg_comm_allgather(ctx: *mut ecg_ctx, d_send: *const c_void, d_recv: *mut c_void, bytes: usize) -> c_int;

@@ -192,6 +192,10 @@ def _install_device_fakes(rank, world, corrupt=False, fail_rank=None):
                                                                      make_id=lambda: bytes(range(128)))
     edist.msm_dist = msm_dist
     edist.fft_dist = fft_dist
+    # what an RCCL communicator of `world` ranks on distinct devices reports
+    edist.comm_info = lambda prog: {"count": world, "rank": rank, "device": rank,
+                                    "pci_bus_id": f"0000:{0x11 + 0x10 * rank:02x}:00.0", "transport": "rccl"}
+    edist.last_exchange_us = lambda prog: 40.0 + rank
     return side
 
 
@@ -250,6 +254,10 @@ def test_bench_main_world2(corrupt):
                               "ntt_dist_2gpu_vs_parallel_fft_2^8": not corrupt}
     assert line["value"] > 0 and line["ntt_dist"]["value"] > 0
     assert line["msm_window_table"]["equals_headline_result"] is True
+    # rank 0's record of what every rank's communicator reported
+    assert line["rccl"] == {"transport": ["rccl"], "count": [2], "ranks": [0, 1],
+                            "devices": ["0000:11:00.0", "0000:21:00.0"], "distinct": True,
+                            "msm_allgather_us": 41.0}
 
 
 @pytest.mark.timeout(300)

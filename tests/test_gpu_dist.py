@@ -24,6 +24,7 @@ import ctypes
 import os
 import sys
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -129,12 +130,24 @@ def test_comm_world1_rccl(gpu_programs):
         e = rand_fr(po.BN254_FR, nb, 6)
         d_b = ecgpu.DeviceBuffer.upload(prog, bases)
         d_e = ecgpu.DeviceBuffer.upload(prog, e)
+        # the first MSM on this context: a workspace failure of its local step
+        # (capped by ecg_ctx_set_mem_limit) still runs the status exchange,
+        # whose staging was reserved at ecg_comm_init
+        prog.set_mem_limit(1 << 12)
+        with pytest.raises(ecgpu.EcError, match="ecg_ctx_set_mem_limit"):
+            edist.msm_dist(prog, "bn254", d_b, d_e, nb)
+        prog.set_mem_limit(0)
         with pytest.raises(ecgpu.EcError, match="unknown curve"):
             edist.msm_dist(prog, 7, d_b, d_e, nb)
         with pytest.raises(ecgpu.Aborted):
             edist.msm_dist(prog, "bn254", d_b, d_e, nb, maybe_abort=lambda: True)
         got = edist.msm_dist(prog, "bn254", d_b, d_e, nb)
         assert (co.jac_to_affine(1, got) == co.jac_to_affine(1, co.multiexp_cpu(1, bases, e, nthreads=8))).all()
+        # what the communicator itself reports (bench.py's `rccl` record at N > 1)
+        info = edist.comm_info(prog)
+        assert info["transport"] == "rccl" and info["count"] == 1 and info["rank"] == 0
+        assert info["device"] == gpu_programs[1][0].index and ":" in info["pci_bus_id"]
+        assert edist.last_exchange_us(prog) > 0
         for buf in (d, d_b, d_e):
             buf.free()
     finally:
@@ -267,6 +280,49 @@ def test_dist_failure_semantics(gpu_programs):
         res = _run_ranks(world, lambda r: edist.fft_dist(progs[r], "bls12_381_fr", blk[r], om, 10))
         assert not any(ok for ok, _ in res)
         for b in d_b + d_e + blk:
+            b.free()
+    finally:
+        for p in progs:
+            p.close()
+
+
+def test_dist_workspace_failure_fails_fast(gpu_programs):
+    """a rank whose local MSM fails on a workspace
+    allocation (here: rank 1 of 3 capped by ecg_ctx_set_mem_limit) still joins
+    the status exchange -- the status records need no allocation after the
+    local step -- so all three ranks return ECG_ERR_NOMEM within seconds, not
+    at the exchange deadline.  comm_info reports the host transport; the same
+    ranks then run a good call exactly."""
+    world = 3
+    dev = gpu_programs[1][0]
+    progs = _host_ranks(dev, world, timeout_s=45)
+    try:
+        cid, cname = 0, "bls12_381"
+        n = 5000
+        B = co.gen_bases(cid, 31, 37, n, 8)
+        E = rand_fr(po.BLS12_381_FR, n, 17)
+        d_b = [ecgpu.DeviceBuffer.upload(p, B) for p in progs]
+        d_e = [ecgpu.DeviceBuffer.upload(p, E) for p in progs]
+        infos = [edist.comm_info(p) for p in progs]
+        assert [i["rank"] for i in infos] == [0, 1, 2] and all(i["count"] == 3 for i in infos)
+        assert all(i["transport"] == "host" for i in infos)
+        rec = edist.comm_record(infos)
+        assert rec["distinct"] is False and rec["ranks"] == [0, 1, 2]  # three ranks on one GPU
+        progs[1].set_mem_limit(1 << 12)
+        t0 = time.perf_counter()
+        res = _run_ranks(world, lambda r: edist.msm_dist(progs[r], cname, d_b[r], d_e[r], n), timeout=120)
+        elapsed = time.perf_counter() - t0
+        assert not any(ok for ok, _ in res), res
+        assert all(f"rc={ecgpu.ECG_ERR_NOMEM}" in str(e) for _, e in res), res
+        assert "ecg_ctx_set_mem_limit" in str(res[1][1])
+        assert "rank 1 of 3 failed" in str(res[0][1]) and "rank 1 of 3 failed" in str(res[2][1])
+        assert elapsed < 15, elapsed
+        progs[1].set_mem_limit(0)
+        res = _run_ranks(world, lambda r: edist.msm_dist(progs[r], cname, d_b[r], d_e[r], n))
+        want = co.jac_to_affine(cid, co.multiexp_cpu(cid, np.concatenate([B] * 3), np.concatenate([E] * 3),
+                                                     nthreads=8))
+        assert all(ok and (co.jac_to_affine(cid, v) == want).all() for ok, v in res), res
+        for b in d_b + d_e:
             b.free()
     finally:
         for p in progs:

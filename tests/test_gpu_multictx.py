@@ -202,6 +202,37 @@ def test_msm_pass_size_from_memory(progs, cname, cid):
 
 
 @pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_host_pipeline_multi_batch(progs, cname, cid):
+    """the pipelined host MSM with more passes than
+    bucket slots (ecg_msm -> msm_host_t).  Passes pinned to 2^12 terms: 2^15 + 37 terms are 9 passes,
+    i.e. a batch of 8 slots and a batch of 1, each with its own reduction
+    (CORE_FIN), the batches folded on the host.  With the context capped at
+    300 MB (ecg_ctx_set_mem_limit) no second bucket slot fits the budget
+    (msm_slot_cap): 9 batches of one slot.  Both equal multiexp_cpu and the
+    resident one-pass MSM."""
+    cv = po.CURVES[cname]
+    n = (1 << 15) + 37
+    B = co.gen_bases(cid, 900 + cid, 5, n, 8)
+    E = rand_scalars(cv, n, 910 + cid)
+    want = co.multiexp_cpu(cid, B, E, nthreads=16)
+    p = progs[1]
+    d_b = ecgpu.DeviceBuffer.upload(p, B)
+    d_e = ecgpu.DeviceBuffer.upload(p, E)
+    assert same(cid, ecgpu.msm_dev(p, cname, d_b, d_e, n), want)
+    k = ecgpu.MultiexpKernel.create([p], [], cname)
+    p.set_msm_chunk(1 << 12)
+    try:
+        assert same(cid, k.multiexp(ecgpu.Worker(), B, E, 0), want)
+        p.set_mem_limit(300 << 20)
+        assert same(cid, k.multiexp(ecgpu.Worker(), B, E, 0), want)
+    finally:
+        p.set_mem_limit(0)
+        p.set_msm_chunk(0)
+        d_b.free()
+        d_e.free()
+
+
+@pytest.mark.parametrize("cname,cid", CURVES)
 def test_msm_multi_pass(progs, cname, cid):
     """Passes forced to 2^12 terms: n = 2^14 + 37 runs as 5 passes (window
     sums folded per pass on the host) and must equal multiexp_cpu; an abort
