@@ -14,12 +14,13 @@
 // independent lanes per launch:
 //   1. ecfft_load      Jacobian (any Z) -> XYZZ, written to bit-reversed slots
 //   2. ecfft_twiddle   omega^i, i < n/2, canonical (scalar-mul bit source); on
-//                      BLS12-381 G1 split into GLV halves k = k1 + k2 LAMBDA
-//                      (phi(x, y) = (BETA x, y) = LAMBDA P on G1): the twiddle
-//                      product becomes a joint 128-bit ladder over
-//                      {P, phi P, P + phi P} -- half the doublings.  Inputs
-//                      must be G1 (prime-order subgroup) points, as ark's
-//                      G1Projective values are.
+//                      G1 split into GLV halves k = k1 + k2 LAMBDA
+//                      (phi(x, y) = (BETA x, y) = LAMBDA P on G1): BLS12-381
+//                      by division by its 128-bit LAMBDA, BN254 by the signed
+//                      lattice split (254-bit LAMBDA); the twiddle product
+//                      becomes two 128-bit products -- half the doublings.
+//                      Inputs must be G1 (prime-order subgroup) points, as
+//                      ark's G1Projective values are.
 //   3. ecfft_stage     log_n launches of n/2 independent radix-2 DIT
 //                      butterflies (A, B) -> (A + wB, A - wB), w = 1
 //                      butterflies skip the multiply.  G1 points run in the
@@ -27,7 +28,13 @@
 //                      in ecfft_load, back in ecfft_store; ~1.5x faster than
 //                      the 32-bit-limb lazy form, which G2 keeps)
 //   4. ecfft_store     XYZZ -> normalised Jacobian (x, y, 1) / (0, 1, 0)
+#include <atomic>
 #include <cstring>
+#include <vector>
+
+#ifndef ECG_INST
+#error "compile with -DECG_INST=<curve id>"
+#endif
 
 #include "ctx.hpp"
 #include "curve.hpp"
@@ -122,8 +129,124 @@ ECG_DEV void glv_split(const uint32_t* k, uint32_t* k1, uint32_t* k2) {
   }
 }
 
+// 32-bit words of a u64 constant array
+template <int N>
+ECG_DEV void words_of(const uint64_t (&v)[N], uint32_t* w) {
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    w[2 * i] = (uint32_t)v[i];
+    w[2 * i + 1] = (uint32_t)(v[i] >> 32);
+  }
+}
+
+// c = floor((k g + 2^319) / 2^320) for k < 2^256 (8 words) and g < 2^256 (8
+// words): the rounded k * (b / r) of the lattice split, c < 2^128
+ECG_DEV void glv_round(const uint32_t* k, const uint32_t* g, uint32_t* c) {
+  uint32_t pr[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) pr[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint64_t t = (uint64_t)k[i] * g[j] + pr[i + j] + carry;
+      pr[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    pr[i + 8] = (uint32_t)carry;
+  }
+  uint64_t t = (uint64_t)pr[9] + 0x80000000u;  // + 2^319
+  pr[9] = (uint32_t)t;
+#pragma unroll
+  for (int i = 10; i < 14; i++) {
+    t = (uint64_t)pr[i] + (t >> 32);
+    c[i - 10] = (uint32_t)t;
+  }
+}
+
+// low 128 bits of x * y (4 words each)
+ECG_DEV void mul_lo128(const uint32_t* x, const uint32_t* y, uint32_t* z) {
+  uint32_t r[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint64_t carry = 0;
+#pragma unroll
+    for (int j = 0; i + j < 4; j++) {
+      const uint64_t t = (uint64_t)x[i] * y[j] + r[i + j] + carry;
+      r[i + j] = (uint32_t)t;
+      carry = t >> 32;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) z[i] = r[i];
+}
+
+ECG_DEV void sub128(uint32_t* x, const uint32_t* y) {  // x -= y mod 2^128
+  uint64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t d = (uint64_t)x[i] - y[i] - br;
+    x[i] = (uint32_t)d;
+    br = (d >> 63) & 1;
+  }
+}
+
+// |v| with the sign in bit 127 (|v| < 2^126: GLV_LATTICE bound)
+ECG_DEV void sign_magnitude128(uint32_t* v) {
+  if (!(v[3] >> 31)) return;
+  const uint32_t z[4] = {0, 0, 0, 0};
+  uint32_t m[4] = {z[0], z[1], z[2], z[3]};
+  sub128(m, v);
+#pragma unroll
+  for (int i = 0; i < 4; i++) v[i] = m[i];
+  v[3] |= 0x80000000u;
+}
+
+// GLV lattice split of k < r (BN254 G1, GLV = 2; constants and bounds in
+// tools/gen_params.py): k = k1 + k2 LAMBDA mod r, each half as a 127-bit
+// magnitude with its sign in bit 127.  Once per twiddle, when the table is
+// built.
+template <class C>
+ECG_DEV void glv_lattice_split(const uint32_t* k, uint32_t* k1, uint32_t* k2) {
+  using G = typename C::Gen;
+  uint32_t g1[8], g2[8], a1[4], a2[4], nb1[4], b2[4], c1[4], c2[4], t[4];
+  words_of(G::G1, g1);
+  words_of(G::G2, g2);
+  words_of(G::A1, a1);
+  words_of(G::A2, a2);
+  words_of(G::NB1, nb1);
+  words_of(G::B2, b2);
+  glv_round(k, g1, c1);
+  glv_round(k, g2, c2);
+#pragma unroll
+  for (int i = 0; i < 4; i++) k1[i] = k[i];
+  mul_lo128(c1, a1, t);
+  sub128(k1, t);
+  mul_lo128(c2, a2, t);
+  sub128(k1, t);
+  mul_lo128(c1, nb1, k2);
+  mul_lo128(c2, b2, t);
+  sub128(k2, t);
+  sign_magnitude128(k1);
+  sign_magnitude128(k2);
+}
+
+// the sign bit of a lattice half (GLV = 2), cleared from k; false otherwise
+template <class C>
+ECG_DEV bool glv_take_sign(uint32_t* k) {
+  if constexpr (C::Gen::GLV == 2) {
+    const bool neg = k[3] >> 31;
+    k[3] &= 0x7fffffffu;
+    return neg;
+  } else {
+    return false;
+  }
+}
+
 // Twiddle table entry i (2 x uint4): canonical omega^i, or its GLV halves
-// (k1 | k2) for curves with the endomorphism.
+// (k1 | k2) for curves with the endomorphism (BLS12-381: by division by the
+// 128-bit LAMBDA; BN254: the lattice split, signed).
 template <class C>
 __global__ void __launch_bounds__(ECFFT_THREADS)
     ecfft_twiddle_kernel(Fp<typename C::FrParams> omega, uint32_t half, uint4* __restrict__ tw) {
@@ -133,7 +256,10 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
   S w = from_mont(fpow_u32(omega, i));
   if constexpr (has_glv<C>()) {
     uint32_t k1[4], k2[4];
-    glv_split<C>(w.v, k1, k2);
+    if constexpr (C::Gen::GLV == 2)
+      glv_lattice_split<C>(w.v, k1, k2);
+    else
+      glv_split<C>(w.v, k1, k2);
     tw[2 * i] = make_uint4(k1[0], k1[1], k1[2], k1[3]);
     tw[2 * i + 1] = make_uint4(k2[0], k2[1], k2[2], k2[3]);
   } else {
@@ -147,13 +273,16 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
 // table {P, phi P, P + phi P} per nonzero bit pair.  The table lives in a
 // per-butterfly global slot (L2-resident), keeping VGPRs for the chain.
 template <class C, class PF>
-ECG_DEV XYZZ<PF> glv_joint_mul(const XYZZ<PF>& P, const uint32_t* k1, const uint32_t* k2, XYZZ<PF>* tab) {
+ECG_DEV XYZZ<PF> glv_joint_mul(const XYZZ<PF>& P0, const uint32_t* k1s, const uint32_t* k2s, XYZZ<PF>* tab) {
   using F = typename C::Fq;
-  if (pa_is_zero(P)) return P;
+  if (pa_is_zero(P0)) return P0;
+  uint32_t k1[4] = {k1s[0], k1s[1], k1s[2], k1s[3]}, k2[4] = {k2s[0], k2s[1], k2s[2], k2s[3]};
+  const bool n1 = glv_take_sign<C>(k1), n2 = glv_take_sign<C>(k2);  // lattice halves are signed
   F beta;
   from_u64_words(beta, C::Gen::BETA);
-  XYZZ<PF> phi = P;
-  phi.X = pa_mul_const(P.X, beta);
+  const XYZZ<PF> P = n1 ? pa_neg(P0) : P0;
+  XYZZ<PF> phi = n2 ? pa_neg(P0) : P0;
+  phi.X = pa_mul_const(P0.X, beta);
   store_xyzz(&tab[0], P);
   store_xyzz(&tab[1], phi);
   store_xyzz(&tab[2], pa_add(P, phi));
@@ -325,10 +454,11 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
     const uint32_t e = j << (log_n - 1 - s);
     if constexpr (glv) {
       const uint4 kk = tw[2 * e + half];
-      const uint32_t k[4] = {kk.x, kk.y, kk.z, kk.w};
+      uint32_t k[4] = {kk.x, kk.y, kk.z, kk.w};
+      const bool kneg = glv_take_sign<C>(k);  // BN254: signed lattice halves (uniform per half)
       typename C::Fq beta;
       from_u64_words(beta, C::Gen::BETA);
-      XYZZ<PF> Bh = B;
+      XYZZ<PF> Bh = neg_if(B, kneg);
       Bh.X = sel_words(half != 0, pa_mul_const(B.X, beta), B.X);  // phi(x, y) = (beta x, y)
       const XYZZ<PF> Rh = win_mul<4, PM>(Bh, k, tabs + (size_t)ECFFT_TAB * g);
       R = pp_add<PM>(Rh, shfl_xor1<1 << PB>(Rh));
@@ -351,12 +481,138 @@ __global__ void __launch_bounds__(ECFFT_THREADS)
   }
 }
 
+// ---------------------------------------------------------------------------
+// Radix-2^d stages (the small transforms, where a stage's cost is its one
+// scalar multiplication's chain, not its work).  One radix-2^d DIT stage does
+// the work of d radix-2 stages with ONE multiplication on its critical path:
+// over bit-reversed input, block blk of M = 2^(s+d) points holds R = 2^d
+// transformed sub-blocks of 2^s points -- sub-block m transforms the inputs
+// congruent to m' = brev_d(m) mod R -- and output j + q 2^s (j < 2^s, q < R)
+// of the block is
+//     sum_{m < R} omega^E(j, m, q) in[blk M + j + m 2^s],
+//     E = (n/M) ((j + q 2^s) m' mod M) = (n/M) j m' + q m' (n/R)  (mod n).
+// E(q + R/2) = E(q) + m' n/2: for odd m' the product is negated, for even m'
+// it is the same, so a stage needs n (R - 1) / 2 distinct products (R = 2: the
+// radix-2 butterfly's n/2).  Kernel 1 computes them (windowed, GLV halves,
+// lane pairs / quads as the radix-2 stage); kernel 2 sums each output's R
+// terms (its m = 0 term is the input itself) into the other point buffer.
+// The work grows as 2 (R - 1) / d over radix-2 stages, the chain shrinks d
+// times; ecfft_radix_plan picks d per size.
+// ---------------------------------------------------------------------------
+struct RadixStage {
+  uint32_t log_n, s, d;
+  uint32_t np;     // distinct products per transform: (n / 2) (R - 1)
+  uint32_t batch;
+};
+
+template <class C, class PF, int PM>
+__global__ void __launch_bounds__(ECFFT_THREADS)
+    ecfft_rprod_kernel(const XYZZ<PF>* __restrict__ a, XYZZ<PF>* __restrict__ prod, const uint4* __restrict__ tw,
+                       RadixStage st, XYZZ<PF>* __restrict__ tabs) {
+  constexpr bool glv = has_glv<C>();
+  constexpr uint32_t PB = pp_lanes_log<PM>();
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t per_op = (glv ? 2u : 1u) << PB;  // lanes per product
+  if (g >= st.batch * st.np * per_op) return;      // the lanes of a product leave together
+  const uint32_t role = g & ((1u << PB) - 1);
+  uint32_t op = g >> PB;
+  const uint32_t half = glv ? (op & 1u) : 0u;
+  if (glv) op >>= 1;
+  const uint32_t tr = op / st.np, t = op - tr * st.np;
+  const uint32_t d = st.d, s = st.s, R1 = (1u << d) - 1;
+  const uint32_t q = t & ((1u << (d - 1)) - 1);
+  const uint32_t u = t >> (d - 1);
+  const uint32_t j = u & ((1u << s) - 1);
+  const uint32_t v = u >> s;
+  const uint32_t blk = v / R1, m = v - blk * R1 + 1;
+  const uint32_t n = 1u << st.log_n, half_n = n >> 1;
+  const uint32_t mr = __brev(m) >> (32 - d);  // sub-block m holds the inputs = brev_d(m) mod R
+  const uint32_t E = (((j * mr) << (st.log_n - s - d)) + ((q * mr) << (st.log_n - d))) & (n - 1);
+  const uint32_t e = E & (half_n - 1);
+  const XYZZ<PF> B = load_xyzz(&a[(size_t)tr * n + (blk << (s + d)) + j + (m << s)]);
+  XYZZ<PF> P = B;
+  if (e != 0) {  // uniform within a product's lanes
+    if constexpr (glv) {
+      const uint4 kk = tw[2 * e + half];
+      uint32_t k[4] = {kk.x, kk.y, kk.z, kk.w};
+      const bool kneg = glv_take_sign<C>(k);
+      typename C::Fq beta;
+      from_u64_words(beta, C::Gen::BETA);
+      XYZZ<PF> Bh = neg_if(B, kneg);
+      Bh.X = sel_words(half != 0, pa_mul_const(B.X, beta), B.X);
+      const XYZZ<PF> Rh = win_mul<4, PM>(Bh, k, tabs + (size_t)ECFFT_TAB * g);
+      P = pp_add<PM>(Rh, shfl_xor1<1 << PB>(Rh));
+    } else {
+      const uint4 lo = tw[2 * e], hi = tw[2 * e + 1];
+      const uint32_t k[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      P = win_mul<8, PM>(B, k, tabs + (size_t)ECFFT_TAB * g);
+    }
+  }
+  if (role == 0 && half == 0) store_xyzz(&prod[(size_t)tr * st.np + t], neg_if(P, E >= half_n));
+}
+
+template <class C, class PF, int PM>
+__global__ void __launch_bounds__(ECFFT_THREADS)
+    ecfft_rsum_kernel(const XYZZ<PF>* __restrict__ a, const XYZZ<PF>* __restrict__ prod, XYZZ<PF>* __restrict__ out,
+                      RadixStage st) {
+  constexpr uint32_t PB = pp_lanes_log<PM>();
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= (st.batch << (st.log_n + PB))) return;
+  const uint32_t op = g >> PB;
+  const uint32_t tr = op >> st.log_n, o = op & ((1u << st.log_n) - 1);
+  const uint32_t d = st.d, s = st.s, R1 = (1u << d) - 1;
+  const uint32_t blk = o >> (s + d), oi = o & ((1u << (s + d)) - 1);
+  const uint32_t j = oi & ((1u << s) - 1), q = oi >> s;
+  const uint32_t qh = q & ((1u << (d - 1)) - 1);
+  const bool upper = q >> (d - 1);
+  const XYZZ<PF>* pr = prod + (size_t)tr * st.np + ((((size_t)blk * R1) << s) << (d - 1));
+  XYZZ<PF> acc = load_xyzz(&a[((size_t)tr << st.log_n) + (blk << (s + d)) + j]);
+  XYZZ<PF> nxt = load_xyzz(&pr[((size_t)j << (d - 1)) + qh]);
+#pragma unroll 1
+  for (uint32_t m = 1; m <= R1; m++) {
+    const XYZZ<PF> cur = nxt;
+    if (m < R1) nxt = load_xyzz(&pr[((((size_t)m << s) + j) << (d - 1)) + qh]);  // one ahead
+    acc = pp_add<PM>(acc, neg_if(cur, upper && ((m >> (d - 1)) & 1)));  // odd brev_d(m)
+  }
+  if ((g & ((1u << PB) - 1)) == 0) store_xyzz(&out[((size_t)tr << st.log_n) + o], acc);
+}
+
 static uint32_t ecfft_pairs_max() {  // A/B: ECG_ECFFT_PAIRS = 0 / 1 (single lanes), 2 (pairs), 4 (quads)
   static const uint32_t v = [] {
     const char* e = getenv("ECG_ECFFT_PAIRS");
     return e ? (uint32_t)strtoul(e, nullptr, 10) : 4u;
   }();
   return v;
+}
+
+// Log-radices of the stages of a 2^log_n transform (batch of `batch`): stages
+// of at most dmax radix-2 rounds each, balanced.  dmax = 1 is the radix-2
+// chain.  A/B: ECG_ECFFT_RADIX pins dmax (1 = radix-2 stages only).
+// ecg_ec_fft_set_radix (process-wide A/B and test knob; 0 = automatic)
+extern std::atomic<int> ecfft_radix_pin;
+#if ECG_INST == 0
+std::atomic<int> ecfft_radix_pin{0};
+#endif
+
+static uint32_t ecfft_radix_max(uint32_t log_n, uint32_t batch) {
+  const int api = ecfft_radix_pin.load(std::memory_order_relaxed);
+  if (api > 0) return (uint32_t)api;
+  static const int pinned = [] {
+    const char* e = getenv("ECG_ECFFT_RADIX");
+    const long v = e ? strtol(e, nullptr, 10) : 0;
+    return v >= 1 && v <= 8 ? (int)v : 0;
+  }();
+  if (pinned) return (uint32_t)pinned;
+  (void)batch;
+  return log_n <= 6 ? log_n : log_n <= 10 ? 5u : log_n <= 12 ? 4u : 1u;
+}
+
+static std::vector<uint32_t> ecfft_radix_plan(uint32_t log_n, uint32_t dmax) {
+  std::vector<uint32_t> plan;
+  if (log_n == 0) return plan;
+  const uint32_t nst = (log_n + dmax - 1) / dmax;
+  for (uint32_t k = 0; k < nst; k++) plan.push_back(log_n / nst + (k < log_n % nst ? 1u : 0u));
+  return plan;
 }
 
 static bool ecfft_win_enabled() {  // A/B switch: ECG_ECFFT_WIN=0 keeps the bit ladders (ecfft_stage_kernel)
@@ -437,6 +693,80 @@ static int ecfft_pf(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t l
     ECG_HIP(hipGetLastError());
   }
   kt_reset(ctx, "ecfft_stage");
+  // radix-2^d stages (see ecfft_rprod_kernel) for the latency-bound sizes
+  if constexpr (!std::is_same<PF, F>::value) {
+    const std::vector<uint32_t> plan = win ? ecfft_radix_plan(log_n, ecfft_radix_max(log_n, batch))
+                                           : std::vector<uint32_t>{};
+    bool radix = false;
+    for (uint32_t d : plan) radix = radix || d > 1;
+    if (radix) {
+      const size_t half_lanes = has_glv<C>() ? 2 : 1;
+      size_t np_max = 0;
+      for (uint32_t d : plan) np_max = std::max(np_max, (size_t)(n / 2) * ((1u << d) - 1));
+      auto widen_for = [&](size_t lanes1) -> uint32_t {
+        return QuadOps<PF>::ok && pmax >= 4 && lanes1 <= ((size_t)1 << 14)  ? 4u
+               : PairOps<PF>::ok && pmax >= 2 && lanes1 <= ((size_t)1 << 15) ? 2u
+                                                                            : 1u;
+      };
+      void *a2, *prod, *tabs;
+      ECG_TRY(ws_get(ctx, "ecfft_pts2", nb * sizeof(XYZZ<PF>), &a2));
+      ECG_TRY(ws_get(ctx, "ecfft_prod", (size_t)batch * np_max * sizeof(XYZZ<PF>), &prod));
+      size_t tab_lanes = 0;  // the widest product launch of the plan
+      for (uint32_t d : plan) {
+        const size_t pl1 = (size_t)batch * (n / 2) * ((1u << d) - 1) * half_lanes;
+        tab_lanes = std::max(tab_lanes, pl1 * widen_for(pl1));
+      }
+      ECG_TRY(ws_get(ctx, "ecfft_rtab", (tab_lanes + 1) * ECFFT_TAB * sizeof(XYZZ<PF>), &tabs));
+      XYZZ<PF>* cur = (XYZZ<PF>*)a;
+      XYZZ<PF>* oth = (XYZZ<PF>*)a2;
+      uint32_t s0 = 0;
+      for (uint32_t d : plan) {
+        if (abort_cb && abort_cb(user)) {  // ec_fft.rs:112-116, once per round
+          (void)hipStreamSynchronize(s);
+          return ECG_ABORTED;
+        }
+        const RadixStage rs{log_n, s0, d, (n / 2) * ((1u << d) - 1), batch};
+        ECG_TRY(kt_begin(ctx, "ecfft_stage", s));
+        const size_t pl1 = (size_t)batch * rs.np * half_lanes;
+        const uint32_t wp = widen_for(pl1);
+        const size_t plan_lanes = pl1 * wp;
+        if (wp == 4) {
+          if constexpr (QuadOps<PF>::ok)
+            hipLaunchKernelGGL((ecfft_rprod_kernel<C, PF, 4>), dim3(ecfft_blocks(plan_lanes)), dim3(ECFFT_THREADS), 0,
+                               s, cur, (XYZZ<PF>*)prod, (const uint4*)tw, rs, (XYZZ<PF>*)tabs);
+        } else if (wp == 2) {
+          if constexpr (PairOps<PF>::ok)
+            hipLaunchKernelGGL((ecfft_rprod_kernel<C, PF, 1>), dim3(ecfft_blocks(plan_lanes)), dim3(ECFFT_THREADS), 0,
+                               s, cur, (XYZZ<PF>*)prod, (const uint4*)tw, rs, (XYZZ<PF>*)tabs);
+        } else {
+          hipLaunchKernelGGL((ecfft_rprod_kernel<C, PF, 0>), dim3(ecfft_blocks(plan_lanes)), dim3(ECFFT_THREADS), 0, s,
+                             cur, (XYZZ<PF>*)prod, (const uint4*)tw, rs, (XYZZ<PF>*)tabs);
+        }
+        ECG_HIP(hipGetLastError());
+        const uint32_t ws = widen_for(nb);
+        if (ws == 4) {
+          if constexpr (QuadOps<PF>::ok)
+            hipLaunchKernelGGL((ecfft_rsum_kernel<C, PF, 4>), dim3(ecfft_blocks(nb * 4)), dim3(ECFFT_THREADS), 0, s,
+                               cur, (const XYZZ<PF>*)prod, oth, rs);
+        } else if (ws == 2) {
+          if constexpr (PairOps<PF>::ok)
+            hipLaunchKernelGGL((ecfft_rsum_kernel<C, PF, 1>), dim3(ecfft_blocks(nb * 2)), dim3(ECFFT_THREADS), 0, s,
+                               cur, (const XYZZ<PF>*)prod, oth, rs);
+        } else {
+          hipLaunchKernelGGL((ecfft_rsum_kernel<C, PF, 0>), dim3(ecfft_blocks(nb)), dim3(ECFFT_THREADS), 0, s, cur,
+                             (const XYZZ<PF>*)prod, oth, rs);
+        }
+        ECG_HIP(hipGetLastError());
+        ECG_TRY(kt_end(ctx, "ecfft_stage", s));
+        std::swap(cur, oth);
+        s0 += d;
+      }
+      hipLaunchKernelGGL((ecfft_store_kernel<C, PF>), dim3(ecfft_blocks(nb)), dim3(ECFFT_THREADS), 0, s,
+                         (const XYZZ<PF>*)cur, (uint32_t)nb, (F*)d_jac);
+      ECG_HIP(hipGetLastError());
+      return ECG_OK;
+    }
+  }
   for (uint32_t st = 0; st < log_n; st++) {
     if (abort_cb && abort_cb(user)) {  // ec_fft.rs:112-116, once per round
       (void)hipStreamSynchronize(s);
@@ -489,6 +819,44 @@ static int ecfft_t(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t lo
   return ecfft_pf<C, typename C::Fq>(ctx, d_jac, omega, log_n, s, abort_cb, user, batch);
 }
 
+// One curve per translation unit (-DECG_INST=<curve id>, as msm_inst.hip), so
+// the four curves' stage kernels build in parallel.
+int ecfft_run_0(ecg_ctx*, void*, const uint64_t*, uint32_t, hipStream_t, ecg_abort_cb, void*, uint32_t);
+int ecfft_run_1(ecg_ctx*, void*, const uint64_t*, uint32_t, hipStream_t, ecg_abort_cb, void*, uint32_t);
+int ecfft_run_2(ecg_ctx*, void*, const uint64_t*, uint32_t, hipStream_t, ecg_abort_cb, void*, uint32_t);
+int ecfft_run_3(ecg_ctx*, void*, const uint64_t*, uint32_t, hipStream_t, ecg_abort_cb, void*, uint32_t);
+
+#if ECG_INST == 0
+#define ECG_ECFFT_INST_FN ecfft_run_0
+using EcfftCurve = BLS12_381;
+#elif ECG_INST == 1
+#define ECG_ECFFT_INST_FN ecfft_run_1
+using EcfftCurve = BN254;
+#elif ECG_INST == 2
+#define ECG_ECFFT_INST_FN ecfft_run_2
+using EcfftCurve = BLS12_381_G2;
+#else
+#define ECG_ECFFT_INST_FN ecfft_run_3
+using EcfftCurve = BN254_G2;
+#endif
+int ECG_ECFFT_INST_FN(ecg_ctx* ctx, void* d_jac, const uint64_t* omega, uint32_t log_n, hipStream_t s,
+                      ecg_abort_cb abort_cb, void* user, uint32_t batch) {
+  return ecfft_t<EcfftCurve>(ctx, d_jac, omega, log_n, s, abort_cb, user, batch);
+}
+
+#if ECG_INST == 0
+}  // namespace ecg
+
+extern "C" int ecg_ec_fft_set_radix(int max_log_radix) {
+  if (max_log_radix < 0 || max_log_radix > 8) {
+    ecg::set_error("ecg_ec_fft_set_radix: %d is outside 0 (automatic) .. 8", max_log_radix);
+    return ECG_ERR_INVALID;
+  }
+  ecg::ecfft_radix_pin.store(max_log_radix, std::memory_order_relaxed);
+  return ECG_OK;
+}
+
+namespace ecg {
 int ecfft_validate(int curve_id, uint32_t log_n) {
   uint32_t two_adicity = 0;
   ECG_TRY(with_curve(curve_id, "ec_fft", [&](auto c) {
@@ -507,8 +875,13 @@ int ecfft_run(ecg_ctx* ctx, int curve_id, void* d_jac, const uint64_t* omega, ui
               ecg_abort_cb abort_cb, void* user, uint32_t batch) {
   ECG_TRY(ecfft_validate(curve_id, log_n));
   if (batch == 0) return ECG_OK;
-  return with_curve(curve_id, "ec_fft",
-                    [&](auto c) { return ecfft_t<decltype(c)>(ctx, d_jac, omega, log_n, s, abort_cb, user, batch); });
+  switch (curve_id) {  // validated above
+    case ECG_CURVE_BLS12_381: return ecfft_run_0(ctx, d_jac, omega, log_n, s, abort_cb, user, batch);
+    case ECG_CURVE_BN254: return ecfft_run_1(ctx, d_jac, omega, log_n, s, abort_cb, user, batch);
+    case ECG_CURVE_BLS12_381_G2: return ecfft_run_2(ctx, d_jac, omega, log_n, s, abort_cb, user, batch);
+    default: return ecfft_run_3(ctx, d_jac, omega, log_n, s, abort_cb, user, batch);
+  }
 }
+#endif
 
 }  // namespace ecg

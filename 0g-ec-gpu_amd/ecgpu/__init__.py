@@ -120,6 +120,7 @@ _SIGS = {
     "ecg_msm_chunk_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "ecg_ctx_set_msm_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
     "ecg_ctx_set_mem_limit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "ecg_ec_fft_set_radix": (ctypes.c_int, [ctypes.c_int]),
     "ecg_comm_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                      ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_size_t,
                                      ctypes.POINTER(ctypes.c_int)]),
@@ -751,6 +752,13 @@ def radix_ec_fft(prog: Program, inp: np.ndarray, omegas, curve="bls12_381") -> N
         raise EcError("radix_ec_fft: input length must be a power of two")
     SingleEcFftKernel(prog, _curve(curve)).radix_ec_fft(inp, np.asarray(omegas, dtype=np.uint64).reshape(-1, 4)[0],
                                                         log_n)
+
+
+def ec_fft_set_radix(max_log_radix: int) -> None:
+    """Largest log2-radix of the EC-FFT stages, process-wide (ecg_ec_fft_set_radix):
+    1 = radix-2 stages only, 0 = the engine's choice per size.  Results never
+    depend on it."""
+    _check(lib().ecg_ec_fft_set_radix(int(max_log_radix)), "ec_fft_set_radix")
 
 
 def ec_fft_dev(prog: Program, curve, d_data: DeviceBuffer, omega: np.ndarray, log_n: int) -> None:

@@ -573,6 +573,69 @@ def main():
             small[str(ls)] = (time.perf_counter() - t_a) * 1e3
             d_s.free()
         aux["ec_fft_small_ms"] = small
+        # the reference's own EC-FFT bench (ag-cuda-ec/benches/ec_fft.rs:20-55): degrees 0..11, one
+        # radix_ec_fft_st call each on host points (its "GPU took {}ms" includes the copies in and out)
+        ek1 = ecgpu.EcFftKernel.create([prog], args.curve)
+        seq = {}
+        for deg in range(0, 12):
+            x = np.ascontiguousarray(jac[:1 << deg])
+            om_d = omega_for(cid, r_int, deg)
+            ek1.radix_ec_fft(x.copy(), om_d, deg)  # first call of a size builds its twiddles
+            best = 1e9
+            for _ in range(3):
+                y = x.copy()
+                t_a = time.perf_counter()
+                ek1.radix_ec_fft(y, om_d, deg)
+                best = min(best, time.perf_counter() - t_a)
+            seq[str(deg)] = best * 1e3
+        aux["reference_ec_fft_bench_sequential_ms"] = {
+            "ms_by_log_n": seq,
+            "note": "benches/ec_fft.rs bench_ec_fft_sequential: one radix_ec_fft per degree 0..11, host points in and "
+                    "out, best of 3 after one warm call"}
+        # benches/ec_fft.rs:62-112 bench_ec_fft_parallel: 32 concurrent tasks, each a forward and an
+        # inverse 2^6 transform on its own thread-local workspace (here: 32 threads, one context each)
+        import threading
+        ln6, tasks = 6, 32
+        om6 = omega_for(cid, r_int, ln6)
+        om6_inv = u64(pow(int(sum(int(v) << (64 * i) for i, v in enumerate(om6))) * pow(1 << 256, -1, r_int)
+                          % r_int, -1, r_int) * (1 << 256) % r_int)
+        tprogs = [ecgpu.program(ecgpu.Device(0 if args.single_device else local_rank)) for _ in range(tasks)]
+        tks = [ecgpu.EcFftKernel.create([tp], args.curve) for tp in tprogs]
+        xs6 = [np.ascontiguousarray(jac[(i << ln6):((i + 1) << ln6)]) for i in range(tasks)]
+
+        def par_round():
+            ys = [x.copy() for x in xs6]
+
+            def task(i):
+                tks[i].radix_ec_fft(ys[i], om6, ln6)
+                tks[i].radix_ec_fft(ys[i], om6_inv, ln6)
+
+            th = [threading.Thread(target=task, args=(i,)) for i in range(tasks)]
+            t_a = time.perf_counter()
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            return time.perf_counter() - t_a, ys
+
+        par_round()
+        par_s, ys6 = min((par_round() for _ in range(3)), key=lambda v: v[0])
+        # forward then inverse = n x the input (the bench's own check, ec_fft.rs:104-108)
+        scale_ok = True
+        n6 = co20.u64arr([1 << ln6], 4)
+        for i in (0, tasks - 1):
+            want6 = [co20.jac_to_affine(cid, co20.naive_multiexp(cid, np.ascontiguousarray(xs6[i][j:j + 1, :2 * lq]),
+                                                                 n6)) for j in range(1 << ln6)]
+            got6 = [co20.jac_to_affine(cid, ys6[i][j]) for j in range(1 << ln6)]
+            scale_ok = scale_ok and all((a is None and b is None) or (a is not None and b is not None and (a == b).all())
+                                        for a, b in zip(want6, got6))
+        for tp in tprogs:
+            tp.close()
+        aux["reference_ec_fft_bench_parallel"] = {
+            "tasks": tasks, "log_n": ln6, "ms": par_s * 1e3, "ms_per_task_pair": par_s * 1e3 / tasks,
+            "forward_inverse_is_n_times_input": bool(scale_ok),
+            "note": "benches/ec_fft.rs bench_ec_fft_parallel: 32 threads, each forward + inverse 2^6 on its own "
+                    "context, host points; wall time of the whole set, best of 3"}
         d_jac.free()
         d_pts.free()
         # radix_ec_fft_many over 16 same-size inputs (the 2^16 points cut into 2^12

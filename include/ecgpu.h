@@ -164,6 +164,11 @@ int ecg_fft_dev(ecg_ctx *ctx, int field_id, void *d_inout, const uint64_t *omega
  * two-adicity); log_n = 0 returns the (normalised) input. */
 int ecg_ec_fft(ecg_ctx *ctx, int curve_id, uint64_t *inout_jac, const uint64_t *omega, uint32_t log_n,
                ecg_abort_cb abort_cb, void *user);
+/* Largest radix (as log2) of the EC-FFT stages, process-wide: 1 = radix-2
+ * stages only, up to 8; 0 (default) = the engine's choice per size (radix-2^d
+ * stages for the small, latency-bound transforms).  Results
+ * never depend on it.  A/B and test knob, as ECG_ECFFT_RADIX. */
+int ecg_ec_fft_set_radix(int max_log_radix);
 /* EcFftKernel::radix_ec_fft_many (ec_fft.rs:224-270): ceil(count / nctx)
  * transforms per context, one host thread per context, first error wins. */
 int ecg_ec_fft_many(ecg_ctx **ctxs, int nctx, int curve_id, uint64_t **inouts, const uint64_t *omegas,

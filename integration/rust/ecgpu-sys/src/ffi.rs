@@ -109,6 +109,7 @@ extern "C" {
     // ---- EC-FFT (ec_fft.rs:56-164, 224-270) ----
     pub fn ecg_ec_fft(ctx: *mut ecg_ctx, curve_id: c_int, inout_jac: *mut u64, omega: *const u64, log_n: u32,
                       abort_cb: ecg_abort_cb, user: *mut c_void) -> c_int;
+    pub fn ecg_ec_fft_set_radix(max_log_radix: c_int) -> c_int;
     pub fn ecg_ec_fft_many(ctxs: *mut *mut ecg_ctx, nctx: c_int, curve_id: c_int, inouts: *mut *mut u64,
                            omegas: *const u64, log_ns: *const u32, count: usize, abort_cb: ecg_abort_cb,
                            user: *mut c_void) -> c_int;

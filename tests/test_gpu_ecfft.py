@@ -53,9 +53,21 @@ def kernels(gpu_programs):
     return {name: ecgpu.EcFftKernel.create(progs, name) for name, _ in CURVES}
 
 
+@pytest.fixture
+def radix():
+    """ecg_ec_fft_set_radix for one test, back to automatic afterwards."""
+    yield ecgpu.ec_fft_set_radix
+    ecgpu.ec_fft_set_radix(0)
+
+
+@pytest.mark.parametrize("max_radix", [0, 1, 3, 8], ids=["auto", "radix2", "radix8", "radix256"])
 @pytest.mark.parametrize("cname,cid", CURVES)
-def test_gpu_ec_fft_consistency(kernels, cname, cid):
-    """tests/ec_fft.rs:33-82: log_d 1..=14 against serial_ec_fft."""
+def test_gpu_ec_fft_consistency(kernels, radix, cname, cid, max_radix):
+    """tests/ec_fft.rs:33-82: log_d 1..=14 against serial_ec_fft, through every
+    stage form: the engine's choice, radix-2 stages only, and radix-2^d stages
+    of at most 2^3 and 2^8 (ecfft_rprod / ecfft_rsum kernels; mixed radices
+    where d does not divide log_d)."""
+    radix(max_radix)
     cv = po.CURVES[cname]
     top = 14 if cid == 0 else 12
     for log_d in range(1, top + 1):
@@ -119,12 +131,14 @@ def test_gpu_ec_fft_many_and_unnormalised_inputs(kernels, cname, cid):
         assert same_points(cid, g, w)
 
 
+@pytest.mark.parametrize("max_radix", [0, 1], ids=["auto", "radix2"])
 @pytest.mark.parametrize("cname,cid", CURVES)
-def test_gpu_ec_fft_equal_and_opposite_points(kernels, cname, cid):
+def test_gpu_ec_fft_equal_and_opposite_points(kernels, radix, cname, cid, max_radix):
     """Inputs whose butterflies add a point to itself and to its negative: all
     P_j equal (stage 0 computes P + P and P - P), and P_j = (-1)^j P.  These
     take the doubling and identity branches of the full add (on G1 the lane-pair
     form, curve_rr.hpp rr_add_x2), against serial_ec_fft."""
+    radix(max_radix)
     cv = po.CURVES[cname]
     lq = cv.fq.limbs64
     for log_d in (1, 4, 6):

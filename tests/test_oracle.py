@@ -202,15 +202,60 @@ def test_kat_construction(cid):
         assert (pi == B[i]).all()
 
 
-def test_glv_constants():
-    """BLS12-381 G1 endomorphism used by the EC-FFT twiddle multiplications
-    (tools/gen_params.py GLV): LAMBDA^2 + LAMBDA + 1 = 0 mod r, BETA^3 = 1 in
-    Fq, and (BETA x, y) = LAMBDA * (x, y) for the generator and another point."""
+def _gen_params():
     import importlib.util
     spec = importlib.util.spec_from_file_location("gen_params", os.path.join(os.path.dirname(GOLDEN), "..", "tools",
                                                                           "gen_params.py"))
     gp = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(gp)
+    return gp
+
+
+def test_bn254_glv_lattice():
+    """BN254 G1 endomorphism and lattice split of the EC-FFT twiddles
+    (tools/gen_params.py GLV_LATTICE, ecfft.hip glv_lattice_split): LAMBDA is
+    a cube root of unity mod r, BETA in Fq, (BETA x, y) = LAMBDA (x, y) on G1;
+    the basis spans the lattice with det r; and the device's split -- rounded
+    products with 2^320-scaled constants, mod-2^128 arithmetic, sign in bit
+    127 -- gives k1 + k2 LAMBDA = k mod r with |k1|, |k2| < 2^126 on edge and
+    random k."""
+    gp = _gen_params()
+    c = po.BN254
+    r, q = c.fr.modulus, c.fq.modulus
+    g = gp.glv_lattice_consts(c, gp.GLV_LATTICE["bn254"])
+    lam, beta = g["lam"], g["beta"]
+    assert (lam * lam + lam + 1) % r == 0 and pow(beta, 3, q) == 1 and beta != 1
+    for k in (1, 0xFEDCBA9876543210):
+        P = po.jac_to_affine(po.scalar_mul((c.gx, c.gy), k, q), q)
+        assert (beta * P[0] % q, P[1]) == po.jac_to_affine(po.scalar_mul(P, lam, q), q)
+    assert g["a1"] * g["b2"] + g["a2"] * g["nb1"] == r
+    # the bound the sign-in-bit-127 layout relies on
+    assert (g["a1"] + g["a2"]) // 2 + 1 < 1 << 126 and (g["nb1"] + g["b2"]) // 2 + 1 < 1 << 126
+    M = (1 << 128) - 1
+
+    def split(k):
+        c1 = (k * g["g1"] + (1 << 319)) >> 320
+        c2 = (k * g["g2"] + (1 << 319)) >> 320
+        k1 = (k - c1 * g["a1"] - c2 * g["a2"]) & M
+        k2 = (c1 * g["nb1"] - c2 * g["b2"]) & M
+        return [v - (1 << 128) if v >> 127 else v for v in (k1, k2)]
+
+    rng = np.random.default_rng(254)
+    ks = [0, 1, 2, r - 1, r - 2, lam, lam + 1, r // 2, (r + 1) // 2, g["a2"], g["nb1"]]
+    ks += [int.from_bytes(rng.bytes(32), "little") % r for _ in range(20000)]
+    w = po.BN254_FR.two_adic_root()
+    ks += [pow(w, i, r) for i in range(1, 2000)]  # twiddles themselves
+    for k in ks:
+        k1, k2 = split(k)
+        assert abs(k1) < 1 << 126 and abs(k2) < 1 << 126, k
+        assert (k1 + k2 * lam - k) % r == 0, k
+
+
+def test_glv_constants():
+    """BLS12-381 G1 endomorphism used by the EC-FFT twiddle multiplications
+    (tools/gen_params.py GLV): LAMBDA^2 + LAMBDA + 1 = 0 mod r, BETA^3 = 1 in
+    Fq, and (BETA x, y) = LAMBDA * (x, y) for the generator and another point."""
+    gp = _gen_params()
     beta, lam = gp.GLV["bls12_381"]
     c = po.BLS12_381
     r, q = c.fr.modulus, c.fq.modulus

@@ -11,7 +11,7 @@ from concurrent.futures import ThreadPoolExecutor
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "0g-ec-gpu_amd")
 UNITS = [("msm_inst.hip", f"-DECG_INST={i}") for i in range(4)] + [
-    (f, "") for f in ("ntt.hip", "ecfft.hip", "prep.hip", "dfft.hip")]
+    ("ecfft.hip", f"-DECG_INST={i}") for i in range(4)] + [(f, "") for f in ("ntt.hip", "prep.hip", "dfft.hip")]
 
 
 def scan(unit):
