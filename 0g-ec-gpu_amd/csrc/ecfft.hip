@@ -603,8 +603,15 @@ static uint32_t ecfft_radix_max(uint32_t log_n, uint32_t batch) {
     return v >= 1 && v <= 8 ? (int)v : 0;
   }();
   if (pinned) return (uint32_t)pinned;
-  (void)batch;
-  return log_n <= 6 ? log_n : log_n <= 10 ? 5u : log_n <= 12 ? 4u : 1u;
+  // by the points of the whole launch (batch x n): below ~2^15 points a stage
+  // costs its chain, so fewer, wider stages win until their (R - 1) / (d / 2)
+  // times larger product count fills the chip.  Measured on both G1 curves
+  // (profiles/r05/ecfft_radix_sweep.log): 2^6 2.2x, 2^10 2.5x, 2^12 2.0x,
+  // 2^14 1.15x over radix-2 stages; 2^15 up and 32 x 2^10 keep radix-2.
+  uint32_t lt = log_n;
+  for (uint32_t b = batch; b > 1; b >>= 1) lt++;
+  const uint32_t d = lt <= 7 ? log_n : lt == 8 ? 4u : lt <= 10 ? 5u : lt == 11 ? 4u : lt == 12 ? 3u : lt <= 14 ? 2u : 1u;
+  return d < log_n ? d : log_n;
 }
 
 static std::vector<uint32_t> ecfft_radix_plan(uint32_t log_n, uint32_t dmax) {
