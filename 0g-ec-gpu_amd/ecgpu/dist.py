@@ -53,8 +53,13 @@ class HostGroup:
     was forged, altered, replayed or reordered is refused (ConnectionError).
 
     The key is ECGPU_HOSTGROUP_KEY when set.  Without it, a single-node launch
-    (LOCAL_WORLD_SIZE == WORLD_SIZE, rank 0 bound to loopback) derives it from
-    the launch (TORCHELASTIC_RUN_ID and the port); a multi-node launch, whose
+    (LOCAL_WORLD_SIZE == WORLD_SIZE, rank 0 bound to loopback) uses a random
+    key: rank 0 writes it, before it listens, into a file of this user's 0700
+    directory ($XDG_RUNTIME_DIR or the temp dir, `ecgpu-<uid>`), each peer reads
+    it once rank 0 has answered its connection, and rank 0 removes it when every
+    rank has joined -- so another local user can neither read the key nor plant
+    one, where a key derived from the launch's public run id and port could be
+    computed by anyone on the host; a multi-node launch, whose
     rank 0 listens on MASTER_ADDR, refuses to start without an explicit key
     (fail closed).  Rank 0 drops connections that fail the handshake, name an
     out-of-range or duplicate rank, or stall, and keeps accepting until every
@@ -76,7 +81,16 @@ class HostGroup:
         self._sess: dict = {}   # peer rank (rank 0) or 0 (peers) -> [session key, send seq, recv seq]
         if world == 1:
             return
+        # the launch key: given, ECGPU_HOSTGROUP_KEY, or (single node) a random key
+        # that rank 0 writes into this user's private directory before it listens
+        # and the peers read once rank 0 has answered them (_key_file)
+        self._key_path = None
         self._key = key if key is not None else _launch_key(port)
+        if self._key is None:
+            self._key_path = _key_file(port)
+            if rank == 0:
+                self._key = os.urandom(32)
+                _write_private(self._key_path, self._key)
         deadline = time.time() + timeout
         if rank == 0:
             ls = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
@@ -101,6 +115,7 @@ class HostGroup:
                     continue
                 peers[r] = c
             self._peers = [peers[r] for r in range(1, world)]
+            self._drop_key_file()
         else:
             while True:
                 try:
@@ -114,6 +129,8 @@ class HostGroup:
             import hmac
 
             c0 = _recv_exact(c, 32)
+            if self._key is None:  # rank 0 wrote it before listening
+                self._key = _read_private(self._key_path)
             c1 = os.urandom(32)
             c.sendall(rank.to_bytes(4, "little") + c1 + _mac(self._key, b"join", c0, c1, rank))
             reply = _recv_exact(c, 34)
@@ -228,14 +245,65 @@ class HostGroup:
         if self._listener is not None:
             self._listener.close()
         self._peers, self._conn, self._listener = [], None, None
+        self._drop_key_file()
+
+    def _drop_key_file(self) -> None:
+        if getattr(self, "_key_path", None) and self.rank == 0:
+            try:
+                os.unlink(self._key_path)
+            except OSError:
+                pass
+            self._key_path = None
 
 
-def _launch_key(port: int) -> bytes:
+def _launch_key(port: int) -> bytes | None:
+    """ECGPU_HOSTGROUP_KEY's key, or None: a single-node launch then uses a
+    random key passed through a file only this user can read (_key_file)."""
     explicit = os.environ.get("ECGPU_HOSTGROUP_KEY")
     if explicit:
         return hashlib.sha256(explicit.encode()).digest()
+    return None
+
+
+def _private_dir() -> str:
+    """This user's 0700 directory for launch keys ($XDG_RUNTIME_DIR or the temp
+    dir): another local user can neither read a key nor plant one."""
+    import stat
+    import tempfile
+
+    base = os.environ.get("XDG_RUNTIME_DIR") or tempfile.gettempdir()
+    d = os.path.join(base, f"ecgpu-{os.getuid()}")
+    os.makedirs(d, mode=0o700, exist_ok=True)
+    st = os.lstat(d)
+    if not stat.S_ISDIR(st.st_mode) or st.st_uid != os.getuid() or st.st_mode & 0o077:
+        raise PermissionError(f"HostGroup: {d} must be a directory private to this user (owner, mode 0700)")
+    return d
+
+
+def _key_file(port: int) -> str:
     run = os.environ.get("TORCHELASTIC_RUN_ID", "")
-    return hashlib.sha256(f"ecgpu-hostgroup|{run}|{port}".encode()).digest()
+    tag = hashlib.sha256(f"ecgpu-hostgroup|{run}|{port}".encode()).hexdigest()[:24]
+    return os.path.join(_private_dir(), f"hostgroup-{tag}.key")
+
+
+def _write_private(path: str, data: bytes) -> None:
+    tmp = f"{path}.{os.getpid()}.tmp"
+    fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
+    try:
+        os.write(fd, data)
+    finally:
+        os.close(fd)
+    os.replace(tmp, path)  # atomic: a reader sees the old key or the new one, never a part
+
+
+def _read_private(path: str) -> bytes:
+    import stat
+
+    st = os.lstat(path)
+    if not stat.S_ISREG(st.st_mode) or st.st_uid != os.getuid() or st.st_mode & 0o077:
+        raise PermissionError(f"HostGroup: launch key {path} is not a private file of this user")
+    with open(path, "rb") as f:
+        return f.read()
 
 
 def _mac(key: bytes, label: bytes, c0: bytes, c1: bytes, rank: int) -> bytes:

@@ -249,3 +249,47 @@ def test_hostgroup_exchange_default_pieces_fit_the_frame_cap():
         t.join(120)
     for r in range(world):
         assert out[r] == b"".join(bytes([16 * q + r]) * nb for q in range(world))
+
+
+def test_single_node_key_is_random_and_private(monkeypatch, tmp_path):
+    """without ECGPU_HOSTGROUP_KEY a single-node launch's key is
+    random (not derivable from the public run id and port), passes through a
+    0600 file in a 0700 per-user directory, and is removed once every rank
+    joined; a key file another user could write is refused."""
+    import stat
+
+    monkeypatch.delenv("ECGPU_HOSTGROUP_KEY", raising=False)
+    monkeypatch.setenv("XDG_RUNTIME_DIR", str(tmp_path))
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    port = _free_port()
+    path = edist._key_file(port)
+    d = os.path.dirname(path)
+    assert stat.S_IMODE(os.stat(d).st_mode) == 0o700
+    out, keys = {}, {}
+
+    def rank(r):
+        g = edist.HostGroup(r, 3, "127.0.0.1", port, timeout=60)
+        keys[r] = g._key
+        out[r] = g.allgather(r * 7)
+        g.close()
+
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    assert out == {0: [0, 7, 14], 1: [0, 7, 14], 2: [0, 7, 14]}
+    assert keys[0] == keys[1] == keys[2] and len(keys[0]) == 32
+    assert keys[0] != edist.hashlib.sha256(f"ecgpu-hostgroup|none|{port}".encode()).digest()
+    assert not os.path.exists(path)  # removed after the handshake
+    # a key file that is group/other-writable is not trusted
+    edist._write_private(path, b"x" * 32)
+    os.chmod(path, 0o644)
+    with pytest.raises(PermissionError, match="private"):
+        edist._read_private(path)
+    os.unlink(path)
+    # a shared (not 0700) key directory is refused
+    os.chmod(d, 0o755)
+    with pytest.raises(PermissionError, match="0700"):
+        edist._private_dir()
+    os.chmod(d, 0o700)
