@@ -65,6 +65,10 @@ struct ecg_ctx {
     size_t bytes = 0;
   };
   std::map<std::string, Buf> ws;
+  // pinned host staging (hws_get): the small D2H copies of results (window
+  // sums, task sums) -- a pageable destination cost ~0.2-0.26 ms of host-side
+  // staging per MSM before the copy started (profiles/r04/msm_2p2*_timeline.txt)
+  std::map<std::string, Buf> hws;
   // FFT twiddle-table cache key
   int tw_fid = -1;
   int tw_variant = 0;
@@ -124,6 +128,9 @@ inline size_t ctx_mem(const ecg_ctx* ctx) {
 // Grow-only named device buffer.
 int ws_get(ecg_ctx* ctx, const char* name, size_t bytes, void** out);
 void ws_release(ecg_ctx* ctx, const char* name);
+// Grow-only named pinned host buffer (hipHostMalloc, mapped: kernels may write
+// it directly through *dev), freed with the context.
+int hws_get(ecg_ctx* ctx, const char* name, size_t bytes, void** out, void** dev = nullptr);
 
 // HIP-event bracket for one launch of a named kernel.
 hipEvent_t ev_take(ecg_ctx* ctx);

@@ -79,6 +79,30 @@ int ws_get(ecg_ctx* ctx, const char* name, size_t bytes, void** out) {
   return ECG_OK;
 }
 
+int hws_get(ecg_ctx* ctx, const char* name, size_t bytes, void** out, void** dev) {
+  auto& b = ctx->hws[name];
+  if (bytes == 0) bytes = 16;
+  if (b.bytes < bytes) {
+    if (b.ptr) {
+      ECG_HIP(hipStreamSynchronize(ctx->stream));  // a queued copy may still target it
+      ECG_HIP(hipHostFree(b.ptr));
+      b.ptr = nullptr;
+      b.bytes = 0;
+    }
+    hipError_t e = hipHostMalloc(&b.ptr, bytes, hipHostMallocMapped);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("pinned host allocation of %zu bytes for '%s' failed: %s", bytes, name, hipGetErrorString(e));
+      b.ptr = nullptr;
+      return ECG_ERR_NOMEM;
+    }
+    b.bytes = bytes;
+  }
+  *out = b.ptr;
+  if (dev) ECG_HIP(hipHostGetDevicePointer(dev, b.ptr, 0));
+  return ECG_OK;
+}
+
 void ws_release(ecg_ctx* ctx, const char* name) {
   auto it = ctx->ws.find(name);
   if (it == ctx->ws.end()) return;
@@ -213,6 +237,8 @@ void ecg_ctx_destroy(ecg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   for (auto& kv : ctx->ws)
     if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+  for (auto& kv : ctx->hws)
+    if (kv.second.ptr) (void)hipHostFree(kv.second.ptr);
   for (auto& kv : ctx->ktimes)
     for (auto& pr : kv.second.pending) {
       (void)hipEventDestroy(pr.first);

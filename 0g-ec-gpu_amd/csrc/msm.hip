@@ -52,11 +52,49 @@ std::map<uintptr_t, PrepEntry> g_prep;  // records' start address -> entry
 std::atomic<uint64_t> g_prep_seq{0x9E3779B97F4A7C15ull};
 }  // namespace
 
+// The header check of a prepared buffer, deferred into the call's stream:
+// prep_check_kernel compares the header with the entry's magic and nonce and
+// writes the verdict into mapped pinned host memory, which the caller reads
+// once the call has synchronised (prepared_confirm).  A synchronous 16-B
+// hipMemcpy of the header before every call cost ~0.2 ms of host-side latency
+// (profiles/r05/msm_2p20_timeline_pinned_d2h.txt: the copy blit 0.2 ms after
+// the previous call's last kernel), 5 % of a 2^20 MSM.
+struct PrepCheck {
+  bool pending = false;
+  uintptr_t start = 0;
+  uint64_t nonce = 0;
+  volatile uint32_t* flag = nullptr;  // 0 = not run, 1 = ours, 2 = stale
+};
+
+__global__ void prep_check_kernel(const uint64_t* __restrict__ hdr, uint64_t magic, uint64_t nonce,
+                                  uint32_t* __restrict__ flag) {
+  if (threadIdx.x == 0) flag[0] = (hdr[0] == magic && hdr[1] == nonce) ? 1u : 2u;
+}
+
+static void prepared_drop(uintptr_t start, uint64_t nonce) {  // freed outside the library
+  std::lock_guard<std::mutex> g(g_prep_mu);
+  auto it = g_prep.find(start);
+  if (it != g_prep.end() && it->second.nonce == nonce) g_prep.erase(it);
+}
+
+// After the stream has synchronised: true if the deferred check found the
+// buffer's own header (or nothing was deferred); false drops the stale entry.
+static bool prepared_confirm(const PrepCheck& chk) {
+  if (!chk.pending) return true;
+  if (*chk.flag == 1u) return true;
+  prepared_drop(chk.start, chk.nonce);
+  return false;
+}
+
 // Is d_bases inside a prepared buffer?  It must then sit on a base boundary,
 // on ctx's device, and cover the n bases the call reads, for the same curve.
+// With `defer` (and a stream), the header is checked on the stream instead of
+// by a synchronous copy; the caller must then call prepared_confirm after its
+// work has synchronised and redo the call as unprepared if it returns false.
 static int prepared_lookup(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n, const char* what,
-                           BaseForm* bf) {
+                           BaseForm* bf, hipStream_t s = nullptr, PrepCheck* defer = nullptr) {
   *bf = BaseForm{};
+  if (defer) *defer = PrepCheck{};
   const uintptr_t a = (uintptr_t)d_bases;
   PrepEntry e;
   uintptr_t start;
@@ -79,12 +117,23 @@ static int prepared_lookup(ecg_ctx* ctx, int curve_id, const void* d_bases, size
   const uintptr_t h0 = start - PREP_HEADER, h1 = start + e.n * e.stride;
   const bool live = hipMemGetAddressRange(&alloc_base, &alloc_size, (hipDeviceptr_t)h0) == hipSuccess &&
                     (uintptr_t)alloc_base <= h0 && h1 <= (uintptr_t)alloc_base + alloc_size;
-  if (!live || hipMemcpy(hdr, (const void*)(start - PREP_HEADER), sizeof hdr, hipMemcpyDeviceToHost) != hipSuccess ||
-      hdr[0] != PREP_MAGIC || hdr[1] != e.nonce) {
+  if (!live) {
     (void)hipGetLastError();
-    std::lock_guard<std::mutex> g(g_prep_mu);
-    auto it = g_prep.find(start);
-    if (it != g_prep.end() && it->second.nonce == e.nonce) g_prep.erase(it);  // freed outside the library
+    prepared_drop(start, e.nonce);
+    return ECG_OK;
+  }
+  if (defer && e.device == ctx->device) {  // header checked on the stream (prep_check_kernel)
+    void *h_flag, *d_flag;
+    ECG_TRY(hws_get(ctx, "prep_check", 16, &h_flag, &d_flag));
+    *(volatile uint32_t*)h_flag = 0u;
+    hipLaunchKernelGGL(prep_check_kernel, dim3(1), dim3(64), 0, s, (const uint64_t*)(start - PREP_HEADER),
+                       PREP_MAGIC, e.nonce, (uint32_t*)d_flag);
+    ECG_HIP(hipGetLastError());
+    *defer = PrepCheck{true, start, e.nonce, (volatile uint32_t*)h_flag};
+  } else if (hipMemcpy(hdr, (const void*)(start - PREP_HEADER), sizeof hdr, hipMemcpyDeviceToHost) != hipSuccess ||
+             hdr[0] != PREP_MAGIC || hdr[1] != e.nonce) {
+    (void)hipGetLastError();
+    prepared_drop(start, e.nonce);
     return ECG_OK;
   }
   if (e.device != ctx->device) {
@@ -148,8 +197,13 @@ int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scala
   const MsmOps* o = msm_ops(curve_id, "multiexp");
   if (!o) return ECG_ERR_INVALID;
   BaseForm bf;
-  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n, "multiexp", &bf));
-  return o->single(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0, bf);
+  PrepCheck chk;
+  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n, "multiexp", &bf, s, &chk));
+  int rc = o->single(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0, bf);
+  (void)hipStreamSynchronize(s);
+  if (rc == ECG_OK && !prepared_confirm(chk))  // released behind the library's back: not our records
+    rc = o->single(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0, BaseForm{});
+  return rc;
 }
 
 uint32_t msm_table_window_auto(int curve_id, size_t n) {
@@ -251,9 +305,15 @@ int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_base
   const MsmOps* o = msm_ops(curve_id, "multiple_multiexp");
   if (!o) return ECG_ERR_INVALID;
   BaseForm bf;
-  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n_bases, "multiple_multiexp", &bf));
-  return o->batch(ctx, d_bases, d_scalars, (uint32_t)n_lines, (uint32_t)n_chunks, line_len, scalar_mont != 0,
-                  window_bits, out_jac, s, bf);
+  PrepCheck chk;
+  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n_bases, "multiple_multiexp", &bf, s, &chk));
+  int rc = o->batch(ctx, d_bases, d_scalars, (uint32_t)n_lines, (uint32_t)n_chunks, line_len, scalar_mont != 0,
+                    window_bits, out_jac, s, bf);
+  (void)hipStreamSynchronize(s);
+  if (rc == ECG_OK && !prepared_confirm(chk))  // released behind the library's back: not our records
+    rc = o->batch(ctx, d_bases, d_scalars, (uint32_t)n_lines, (uint32_t)n_chunks, line_len, scalar_mont != 0,
+                  window_bits, out_jac, s, BaseForm{});
+  return rc;
 }
 
 int point_sum_host(int curve_id, const uint64_t* points, size_t count, uint64_t* out_jac) {

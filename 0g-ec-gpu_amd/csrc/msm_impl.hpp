@@ -1404,7 +1404,16 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     }
     if (bits) npts = groups;
     void* st;
-    ECG_TRY(ws_get(ctx, "msm_sums_std", (size_t)npts * sizeof(XYZZ<typename C::Fq>), &st));
+    if (bits) {
+      // single MSMs: the window sums go straight into mapped pinned host memory
+      // (the host folds them next).  A device buffer and a D2H copy left
+      // ~0.2 ms between this kernel and the copy's blit at every size
+      // (profiles/r04/msm_2p20_timeline.txt, profiles/r05/trace20).
+      void* host;
+      ECG_TRY(hws_get(ctx, "msm_sums_host", (size_t)npts * sizeof(XYZZ<typename C::Fq>), &host, &st));
+    } else {
+      ECG_TRY(ws_get(ctx, "msm_sums_std", (size_t)npts * sizeof(XYZZ<typename C::Fq>), &st));
+    }
     hipLaunchKernelGGL((msm_sums_to_std_kernel<F, typename C::Fq>), dim3(blocks_for(npts, 64)), dim3(64), 0, s,
                        (const X*)in, npts, (XYZZ<typename C::Fq>*)st);
     ECG_HIP(hipGetLastError());
@@ -1654,12 +1663,15 @@ void msm_host_fold_bits(const XYZZ<typename C::Fq>* sums, const MsmPlan& e, host
     HostPool::get().parallel_for(nw, [&](size_t w) { window((uint32_t)w); });
   else
     for (uint32_t w = 0; w < nw; w++) window(w);
-  HX acc = HX::zero();
+  // Horner over the windows: c (W - 1) serial doublings, in Jacobian form
+  // (2M + 5S each instead of XYZZ's 6M + 3S)
+  using HJ = host::HJac<HostF<C>>;
+  HJ acc = HJ::zero();
   for (int w = (int)nw - 1; w >= 0; w--) {
-    for (uint32_t k = 0; k < e.c; k++) acc = host::hdbl(acc);
-    acc = host::hadd_pts(acc, win[w]);
+    for (uint32_t k = 0; k < e.c; k++) acc = host::hjac_dbl(acc);
+    acc = host::hjac_add(acc, host::hjac_from_xyzz(win[w]));
   }
-  total = host::hadd_pts(total, acc);
+  total = host::hadd_pts(total, host::hxyzz_from_jac(acc));
 }
 
 // Terms per device pass: calc_chunk_size (multiexp.rs:71-93) restated for
@@ -1712,7 +1724,6 @@ int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_
   using HX = host::HPoint<HostF<C>>;
   kt_reset(ctx, "msm_accumulate");
   HX total_acc = HX::zero();
-  std::vector<X> win;
   const size_t chunk = msm_pass_terms<C>(ctx);
   for (size_t off = 0; off < n; off += chunk) {
     if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144
@@ -1727,10 +1738,12 @@ int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_
     ECG_TRY(msm_core_t<C>(ctx, bp, (const uint4*)d_scalars + 2 * off, g, pl, s, &d_sums, prepared));
     // window A / offset-bit sums -> host; Horner fold over windows (multiexp.rs:221-233)
     const MsmPlan e = msm_eff_plan<C>(pl);
-    win.resize(msm_single_sums(e));
-    ECG_HIP(hipMemcpyAsync(win.data(), d_sums, win.size() * sizeof(X), hipMemcpyDeviceToHost, s));
+    const size_t nw = msm_single_sums(e);
+    // the sums are in mapped host memory already (msm_sums_to_std_kernel)
+    X* win;
+    ECG_TRY(hws_get(ctx, "msm_sums_host", nw * sizeof(X), (void**)&win));
     ECG_HIP(hipStreamSynchronize(s));
-    msm_host_fold_bits<C>(win.data(), e, total_acc);
+    msm_host_fold_bits<C>(win, e, total_acc);
   }
   host::hto_jac_norm(total_acc, out_jac);
   return ECG_OK;
@@ -1893,16 +1906,17 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
       if (last_of_batch) {  // one reduction over the batch's slots
         ECG_TRY(msm_core_t<C>(ctx, bp, is[b], g, pl, cs, &d_sums, resident, nullptr, CORE_FIN,
                               MsmSlots{0, slot + 1}));
-        ECG_HIP(hipMemcpyAsync((X*)sums + batch * nsums, d_sums, nsums * sizeof(X), hipMemcpyDeviceToDevice, cs));
+        ECG_HIP(hipMemcpyAsync((X*)sums + batch * nsums, d_sums, nsums * sizeof(X), hipMemcpyDefault, cs));
       }
       return ECG_OK;
     }();
   }
   (void)hipStreamSynchronize(us);
-  std::vector<X> win(nbatch * nsums);
+  X* win = nullptr;
   if (rc == ECG_OK) {
     rc = [&]() -> int {
-      ECG_HIP(hipMemcpyAsync(win.data(), sums, win.size() * sizeof(X), hipMemcpyDeviceToHost, cs));
+      ECG_TRY(hws_get(ctx, "msm_win", nbatch * nsums * sizeof(X), (void**)&win));  // pinned
+      ECG_HIP(hipMemcpyAsync(win, sums, nbatch * nsums * sizeof(X), hipMemcpyDeviceToHost, cs));
       ECG_HIP(hipStreamSynchronize(cs));
       return ECG_OK;
     }();
@@ -1916,7 +1930,7 @@ int msm_host_t(ecg_ctx* ctx, const void* bases, BaseForm bf, const void* h_scala
   if (rc != ECG_OK) return rc;
   HX total = HX::zero();
   const MsmPlan e = msm_eff_plan<C>(pl);
-  for (size_t k = 0; k < nbatch; k++) msm_host_fold_bits<C>(win.data() + k * nsums, e, total);
+  for (size_t k = 0; k < nbatch; k++) msm_host_fold_bits<C>(win + k * nsums, e, total);
   host::hto_jac_norm(total, out_jac);
   return ECG_OK;
 }
@@ -1965,8 +1979,9 @@ int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const 
     // chain of its own
     using HF = HostF<C>;
     using HX = host::HPoint<HF>;
-    std::vector<XYZZ<F>> sums(tasks);
-    ECG_HIP(hipMemcpyAsync(sums.data(), d_sums, (size_t)tasks * sizeof(XYZZ<F>), hipMemcpyDeviceToHost, s));
+    XYZZ<F>* sums;  // pinned staging
+    ECG_TRY(hws_get(ctx, "msm_task_sums", (size_t)tasks * sizeof(XYZZ<F>), (void**)&sums));
+    ECG_HIP(hipMemcpyAsync(sums, d_sums, (size_t)tasks * sizeof(XYZZ<F>), hipMemcpyDeviceToHost, s));
     ECG_HIP(hipStreamSynchronize(s));
     std::vector<HX> pts(tasks);
     std::vector<HF> pre(tasks);
@@ -2009,8 +2024,11 @@ int msm_batch_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, const 
   hipLaunchKernelGGL(msm_fold_kernel<C>, dim3(blocks_for(tasks, 64)), dim3(64), 0, s, (const XYZZ<F>*)d_sums, pf,
                      tasks, (F*)d_out);
   ECG_HIP(hipGetLastError());
-  ECG_HIP(hipMemcpyAsync(out_jac, d_out, ob, hipMemcpyDeviceToHost, s));
+  void* h_out;  // pinned staging, then the caller's buffer
+  ECG_TRY(hws_get(ctx, "msm_batch_out", ob, &h_out));
+  ECG_HIP(hipMemcpyAsync(h_out, d_out, ob, hipMemcpyDeviceToHost, s));
   ECG_HIP(hipStreamSynchronize(s));
+  memcpy(out_jac, h_out, ob);
   return ECG_OK;
 }
 

@@ -50,6 +50,11 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s
 # v_mad_u64_u32 issue peak: 256 CUs x 4 SIMDs x 16 lanes per cycle (one wave64
 # VALU instruction per 4 cycles per SIMD) at the 2.4 GHz peak clock
 MAD_PEAK_T = 256 * 4 * 16 * 2.4e9 / 1e12
+# measured int-MAD issue rate ("against a *measured* int-MAD peak"): a dependent-free
+# stream of v_mad_u64_u32 issues one wave64 instruction per 4.5 SIMD cycles at 4 waves/SIMD
+# (tools/issue_bench.hip, profiles/r02f/issue_bench.log), i.e. 256 x 4 x 64 / 4.5 per cycle
+MAD_ISSUE_CYCLES = 4.5
+MAD_PEAK_MEASURED_T = 256 * 4 * 64 / MAD_ISSUE_CYCLES * 2.4e9 / 1e12
 R_BLS = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 R_BN = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
 P_BLS = int("1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab", 16)
@@ -718,6 +723,9 @@ def main():
         achieved = n_acc * W * mads / (acc_avg_ms / 1e3) / 1e12
         roofline.update({"achieved": achieved, "peak": MAD_PEAK_T, "unit": "T v_mad_u64_u32/s",
                          "frac": achieved / MAD_PEAK_T,
+                         "measured_peak": {"peak": MAD_PEAK_MEASURED_T, "frac": achieved / MAD_PEAK_MEASURED_T,
+                                           "note": f"{MAD_ISSUE_CYCLES} SIMD cycles per wave64 v_mad_u64_u32 "
+                                                   "(tools/issue_bench.hip) at 2.4 GHz"},
                          "note": f"{mads} v_mad_u64_u32 per XYZZ mixed add (8M+2S, {RR_LIMBS[cid]} x {RR_BITS[cid]}-bit limbs) "
                                  f"x {W} windows x terms / launch time; peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz"})
     roofline["hbm"] = {"achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -196,6 +196,26 @@ def test_prepared_registry_across_contexts_and_views(prog):
         raw_view.ptr = None
         assert same(cid, out, want)
     d_raw.free()
+    # deterministic form of the reuse (the allocator may not hand the address
+    # back): a live prepared allocation whose header and records another owner
+    # overwrote with raw [x, y] bases.  The header is checked on the stream
+    # (msm.hip prep_check_kernel); the mismatch is found after the call, the
+    # entry dropped and the call redone over the raw bases -- same result
+    pb4 = ecgpu.prepare_bases(prog, cname, d_b, n)
+    ptr4 = pb4.ptr.value
+    prog.synchronize()
+    raw = np.ascontiguousarray(np.concatenate([np.zeros(hdr // 8, np.uint64), B.reshape(-1)]))
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(ctypes.c_void_p(ptr4 - hdr), raw.ctypes.data_as(ctypes.c_void_p), raw.nbytes, 1) == 0
+    view4 = ecgpu.PreparedBases(prog, ctypes.c_void_p(ptr4), cid, n)
+    for _ in range(2):  # the second call finds no entry: a plain raw-bases MSM
+        out = np.zeros(18, np.uint64)
+        ecgpu._check(ecgpu.lib().ecg_msm_dev(prog.handle, cid, view4.ptr, d_e.ptr, n,
+                                             out.ctypes.data_as(ctypes.c_void_p), 0, None))
+        assert same(cid, out, want)
+    view4.ptr = None
+    assert hip.hipFree(ctypes.c_void_p(ptr4 - hdr)) == 0
+    pb4.ptr = None
     # the same, with a reused allocation that starts AT the old records address
     # (the old header address is then outside it, or unmapped): the lookup must
     # not read the header there, and the address reads as raw bases
