@@ -710,10 +710,12 @@ def main():
     acc_traffic, acc_src = pmc_traffic("msm_accumulate") if default_run else (None, None)
     if cid == 1 and args.msm_log == 26 and world == 1:  # BN254 (config 5): its own committed PMC pass
         bn = os.path.join(ROOT, "profiles", "pmc_bn254_current.json")  # copy of profiles/r05/pmc_bn254_accumulate.json
-        if os.path.exists(bn):
+        try:
             with open(bn) as f:
                 d_bn = json.load(f)
             acc_traffic, acc_src = d_bn["traffic_gb_per_launch"], d_bn["source"]
+        except (OSError, ValueError, KeyError, TypeError) as e:
+            print(f"bench: ignoring {bn}: {type(e).__name__}: {e}", file=sys.stderr)
     ntt_traffic, ntt_src = pmc_traffic("ntt_pass") if default_run else (None, None)
     ntt_achieved = 64 * n_ntt / (pass_avg_ms / 1e3) / 1e9
     roofline = {"bound": "valu", "kernel": "msm_accumulate", "avg_ms": acc_avg_ms,
@@ -813,13 +815,16 @@ def pmc_traffic(kernel: str):
     path = os.path.join(ROOT, "profiles", "pmc_current.json")
     if not os.path.exists(path):
         return None, None
-    with open(path) as f:
-        d = json.load(f)
-    for k, v in d["kernels"].items():
-        if kernel in k:
-            fetch = v["FETCH_SIZE"]["mean_kb"] * 1024 / 1e9
-            write = v["WRITE_SIZE"]["mean_kb"] * 1024 / 1e9
-            return 2 * fetch + write, d["source"]
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        for k, v in d["kernels"].items():
+            if kernel in k:
+                fetch = v["FETCH_SIZE"]["mean_kb"] * 1024 / 1e9
+                write = v["WRITE_SIZE"]["mean_kb"] * 1024 / 1e9
+                return 2 * fetch + write, d["source"]
+    except (OSError, ValueError, KeyError, TypeError) as e:  # a malformed record must not sink the bench line
+        print(f"bench: ignoring {path}: {type(e).__name__}: {e}", file=sys.stderr)
     return None, None
 
 

@@ -18,6 +18,7 @@
   per-rank partial comes from the CPU oracle instead of ecg_msm_dist.
 * test_msm_sharded_gloo_world2: the same split through torch.distributed over
   gloo (ecgpu.dist.msm_sharded / torch_broadcast)."""
+import json
 import os
 import socket
 import sys
@@ -299,6 +300,20 @@ def test_kat_scalar_regeneration_matches_single_rank():
     k1 = bench.msm_kat_scalar(co, 0, world, n, bench.R_BLS, 2)
     k2 = co.kat_scalar(0, bench.KAT_A, bench.KAT_B, allsc, nthreads=2)
     assert k1 == k2
+
+
+def test_bench_reads_committed_pmc_records():
+    """The committed PMC summaries the default bench line quotes as
+    roofline.traffic parse (a reshaped file once sank a round-end bench)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for kernel in ("msm_accumulate", "ntt_pass"):
+        gb, src = bench.pmc_traffic(kernel)
+        assert gb is not None and gb > 0 and src.startswith("profiles/"), kernel
+    with open(os.path.join(ROOT, "profiles", "pmc_bn254_current.json")) as f:
+        d = json.load(f)
+    assert d["traffic_gb_per_launch"] > 0 and d["source"].startswith("profiles/")
 
 
 def _gloo_worker(rank, world, port, q):
