@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "ctx.hpp"
+#include "msm_ops.hpp"
 
 namespace ecg {
 
@@ -261,6 +262,48 @@ int comm_agree(ecg_ctx* ctx, int local_rc, const uint64_t* agree, int n_agree, c
   return ECG_OK;
 }
 
+// The per-rank [status | curve | partial] records are all-gathered and, when
+// every rank succeeded, the partials folded, so every rank returns the full
+// result -- or the same error (the lowest failing rank's).  `rc` and the
+// partial in rec come from this rank's local step; nothing here allocates
+// (comm_exchange_rec), so a failed local step still joins the exchange.
+static int dist_fold_partials(ecg_ctx* ctx, int rc, int curve_id, uint64_t* rec, size_t rec_words, uint64_t* out_jac,
+                              hipStream_t s, const char* what) {
+  const std::string local_msg = rc != ECG_OK ? last_error_text() : "";
+  if (rc != ECG_OK) (void)hipStreamSynchronize(s);  // the failed run's work is done or abandoned
+  rec[0] = (uint64_t)(int64_t)rc;
+  rec[1] = (uint64_t)(uint32_t)curve_id;
+  const int P = ctx->comm_size;
+  // one exchange, no allocation on this path: every rank joins it whatever
+  // its local step did (comm_exchange_rec)
+  std::vector<uint64_t> all(rec_words * (size_t)P);
+  const auto t_x = std::chrono::steady_clock::now();
+  ECG_TRY(comm_exchange_rec(ctx, rec, all.data(), rec_words * 8, s, what));
+  ctx->comm_last_xchg_us =
+      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_x).count();
+  for (int r = 0; r < P; r++) {  // the lowest failing rank's code, on every rank
+    const int rrc = (int)(int64_t)all[(size_t)r * rec_words];
+    if (rrc == ECG_OK) continue;
+    if (r == ctx->comm_rank)
+      set_error("%s", local_msg.c_str());
+    else
+      set_error("%s: rank %d of %d failed (rc=%d); every rank stops", what, r, P, rrc);
+    return rrc;
+  }
+  const size_t pw = 3 * (size_t)fq_limbs64(curve_id);
+  std::vector<uint64_t> parts(pw * P);
+  for (int r = 0; r < P; r++) {
+    if ((int)all[(size_t)r * rec_words + 1] != curve_id) {
+      set_error("%s: rank %d ran curve %d, this rank curve %d", what, r, (int)all[(size_t)r * rec_words + 1],
+                curve_id);
+      return ECG_ERR_INVALID;
+    }
+    memcpy(&parts[pw * r], &all[(size_t)r * rec_words + 2], pw * 8);
+  }
+  ECG_TRY(point_sum_host(curve_id, parts.data(), (size_t)P, out_jac));  // multiexp.rs:394-397
+  return kt_collect(ctx);
+}
+
 }  // namespace ecg
 
 using namespace ecg;
@@ -399,15 +442,15 @@ int ecg_comm_alltoall(ecg_ctx* ctx, const void* d_send, void* d_recv, size_t byt
   return comm_wait(ctx, ctx->stream, "ecg_comm_alltoall");
 }
 
-// MSM over this rank's shard; the per-rank [status | curve | partial] records
-// are all-gathered and, when every rank succeeded, the partials folded, so
-// every rank returns the full result -- or the same error.
+
+// MSM over this rank's shard (range split), then dist_fold_partials.
 int ecg_msm_dist_ex(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n_local,
                     uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
   ECG_ENTER(ctx);
   hipStream_t s = ctx->stream;
   constexpr size_t PW = 3 * (size_t)ECG_MAX_COORD_U64;  // partial words, the largest curve's
   uint64_t rec[2 + PW] = {};
+  static_assert(sizeof rec <= REC_MAX_BYTES, "MSM status record exceeds the reserved staging");
   int rc = ECG_OK;
   if (!out_jac || ((!d_bases || !d_scalars) && n_local)) {
     set_error("ecg_msm_dist: null pointer");
@@ -425,39 +468,62 @@ int ecg_msm_dist_ex(ecg_ctx* ctx, int curve_id, const void* d_bases, const void*
     memcpy(out_jac, rec + 2, 3 * (size_t)fq_limbs64(curve_id) * 8);
     return kt_collect(ctx);
   }
-  const std::string local_msg = rc != ECG_OK ? last_error_text() : "";
-  if (rc != ECG_OK) (void)hipStreamSynchronize(s);  // the failed run's work is done or abandoned
-  rec[0] = (uint64_t)(int64_t)rc;
-  rec[1] = (uint64_t)(uint32_t)curve_id;
-  const int P = ctx->comm_size;
-  static_assert(sizeof rec <= REC_MAX_BYTES, "MSM status record exceeds the reserved staging");
-  // one exchange, no allocation on this path: every rank joins it whatever
-  // its local step did (comm_exchange_rec)
-  std::vector<uint64_t> all((2 + PW) * (size_t)P);
-  const auto t_x = std::chrono::steady_clock::now();
-  ECG_TRY(comm_exchange_rec(ctx, rec, all.data(), sizeof rec, s, "ecg_msm_dist"));
-  ctx->comm_last_xchg_us =
-      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_x).count();
-  for (int r = 0; r < P; r++) {  // the lowest failing rank's code, on every rank
-    const int rrc = (int)(int64_t)all[(size_t)r * (2 + PW)];
-    if (rrc == ECG_OK) continue;
-    if (r == ctx->comm_rank)
-      set_error("%s", local_msg.c_str());
-    else
-      set_error("ecg_msm_dist: rank %d of %d failed (rc=%d); every rank stops", r, P, rrc);
-    return rrc;
+  return dist_fold_partials(ctx, rc, curve_id, rec, 2 + PW, out_jac, s, "ecg_msm_dist");
+}
+
+// Grid split: every rank holds all n bases and scalars; rank r runs the r-th
+// of comm_size equal ranges of the (window x term) grid of the n-term plan
+// (msm_grid_run), then dist_fold_partials.
+int ecg_msm_dist_grid_ex(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n,
+                         uint64_t* out_jac, ecg_abort_cb abort_cb, void* user) {
+  ECG_ENTER(ctx);
+  hipStream_t s = ctx->stream;
+  constexpr size_t PW = 3 * (size_t)ECG_MAX_COORD_U64;
+  uint64_t rec[2 + PW] = {};
+  int rc = ECG_OK;
+  if (!out_jac || ((!d_bases || !d_scalars) && n)) {
+    set_error("ecg_msm_dist_grid: null pointer");
+    rc = ECG_ERR_INVALID;
+  } else if (!curve_valid(curve_id)) {
+    set_error("multiexp: unknown curve_id %d", curve_id);
+    rc = ECG_ERR_INVALID;
+  } else if (abort_cb && abort_cb(user)) {
+    rc = ECG_ABORTED;
+  } else {
+    kt_reset(ctx, "msm_accumulate");
+    rc = msm_grid_run(ctx, curve_id, d_bases, d_scalars, n, ctx->comm_rank, ctx->comm_size, rec + 2, s, abort_cb,
+                      user, nullptr);
   }
-  const size_t pw = 3 * (size_t)fq_limbs64(curve_id);
-  std::vector<uint64_t> parts(pw * P);
-  for (int r = 0; r < P; r++) {
-    if ((int)all[(size_t)r * (2 + PW) + 1] != curve_id) {
-      set_error("ecg_msm_dist: rank %d ran curve %d, this rank curve %d", r, (int)all[(size_t)r * (2 + PW) + 1],
-                curve_id);
-      return ECG_ERR_INVALID;
-    }
-    memcpy(&parts[pw * r], &all[(size_t)r * (2 + PW) + 2], pw * 8);
+  if (ctx->comm_size == 1 && !ctx->comm) {
+    if (rc != ECG_OK) return rc;
+    memcpy(out_jac, rec + 2, 3 * (size_t)fq_limbs64(curve_id) * 8);
+    return kt_collect(ctx);
   }
-  ECG_TRY(point_sum_host(curve_id, parts.data(), (size_t)P, out_jac));  // multiexp.rs:394-397
+  return dist_fold_partials(ctx, rc, curve_id, rec, 2 + PW, out_jac, s, "ecg_msm_dist_grid");
+}
+
+int ecg_msm_dist_grid(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n,
+                      uint64_t* out_jac) {
+  return ecg_msm_dist_grid_ex(ctx, curve_id, d_bases, d_scalars, n, out_jac, nullptr, nullptr);
+}
+
+// One grid piece set of rank `rank` of `nranks` on this context (no
+// exchange): the per-rank step of ecg_msm_dist_grid, for callers (and tests
+// with several contexts on one device) that fold the partials themselves.
+int ecg_msm_grid_part(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, int rank,
+                      int nranks, uint64_t* out_jac, int* pieces) {
+  ECG_ENTER(ctx);
+  if (!out_jac || ((!d_bases || !d_scalars) && n)) {
+    set_error("ecg_msm_grid_part: null pointer");
+    return ECG_ERR_INVALID;
+  }
+  if (!curve_valid(curve_id)) {
+    set_error("multiexp: unknown curve_id %d", curve_id);
+    return ECG_ERR_INVALID;
+  }
+  kt_reset(ctx, "msm_accumulate");
+  ECG_TRY(msm_grid_run(ctx, curve_id, d_bases, d_scalars, n, rank, nranks, out_jac, ctx->stream, nullptr, nullptr,
+                       pieces));
   return kt_collect(ctx);
 }
 

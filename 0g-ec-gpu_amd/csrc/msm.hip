@@ -206,6 +206,69 @@ int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scala
   return rc;
 }
 
+int msm_grid_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, int rank,
+                 int nranks, uint64_t* out_jac, hipStream_t s, ecg_abort_cb abort_cb, void* user, int* pieces) {
+  if (pieces) *pieces = 0;
+  if (n > 0x7fffffffull) {
+    set_error("multiexp: at most 2^31-1 terms per call");
+    return ECG_ERR_INVALID;
+  }
+  if (nranks < 1 || rank < 0 || rank >= nranks) {
+    set_error("msm_dist_grid: rank %d of %d", rank, nranks);
+    return ECG_ERR_INVALID;
+  }
+  const MsmOps* o = msm_ops(curve_id, "multiexp");
+  if (!o) return ECG_ERR_INVALID;
+  uint32_t c = 0, W = 0;
+  int mode = 0;
+  ECG_TRY(o->plan_info(n ? n : 1, 0, &c, &W, &mode));
+  BaseForm bf;
+  PrepCheck chk;
+  ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n, "multiexp", &bf, s, &chk));
+  if (bf.tab_c) {
+    set_error("msm_dist_grid: the bases are a window table; the grid split needs plain prepared or [x, y] bases");
+    return ECG_ERR_INVALID;
+  }
+  const size_t lq = fq_limbs64(curve_id);
+  // grid entries e = w n + t (window-major); this rank's range [a, b)
+  const unsigned __int128 T = (unsigned __int128)W * n;
+  const uint64_t a = (uint64_t)(T * (unsigned)rank / (unsigned)nranks);
+  const uint64_t b = (uint64_t)(T * (unsigned)(rank + 1) / (unsigned)nranks);
+  auto run = [&](BaseForm f) -> int {
+    const size_t stride = f.prepared ? msm_prepared_stride(curve_id, 0) : 2 * lq * 8;
+    std::vector<uint64_t> parts;
+    int np = 0;
+    uint64_t e = a;
+    while (e < b) {
+      if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144, per device pass
+      const uint32_t w = (uint32_t)(e / n);
+      const size_t t0 = (size_t)(e - (uint64_t)w * n);
+      uint32_t nwin = 1;
+      size_t t1 = n;
+      if (t0 == 0) {  // whole windows run as one piece (one core call, W = nwin groups)
+        nwin = (uint32_t)((b - e) / n);
+        if (nwin == 0) {
+          nwin = 1;
+          t1 = (size_t)(b - e);
+        }
+      } else if (b - (uint64_t)w * n < n) {
+        t1 = (size_t)(b - (uint64_t)w * n);
+      }
+      parts.resize(parts.size() + 3 * lq);
+      ECG_TRY(o->piece(ctx, (const uint8_t*)d_bases + t0 * stride, (const uint8_t*)d_scalars + t0 * 32, t1 - t0, n,
+                       w, nwin, parts.data() + parts.size() - 3 * lq, s, f));
+      np++;
+      e = (uint64_t)(w + nwin - 1) * n + t1;
+    }
+    if (pieces) *pieces = np;
+    return o->point_sum(parts.data(), (size_t)np, out_jac);
+  };
+  int rc = run(bf);
+  (void)hipStreamSynchronize(s);
+  if (rc == ECG_OK && !prepared_confirm(chk)) rc = run(BaseForm{});  // stale: the pointer holds [x, y] bases
+  return rc;
+}
+
 uint32_t msm_table_window_auto(int curve_id, size_t n) {
   const MsmOps* o = msm_ops(curve_id, "prepare_table");
   return o ? o->table_auto(n) : 0;

@@ -151,7 +151,13 @@ struct MsmPlan {
   uint32_t seg;   // sorted entries per accumulation thread
   uint32_t G;     // bucket groups = tasks * W  (one group per (task, window)); tasks with a window table
   uint32_t tab;   // window-table mode: bases in the table (0 = off); every window shares its task's buckets
+  // window pieces (msm_piece_t, the grid split of ecg_msm_dist_grid): the
+  // digits run over wd windows (the carry chain of the whole scalar) and only
+  // windows [w0, w0 + W) are emitted; wd = 0 means W (every window)
+  uint32_t wd;
+  uint32_t w0;
   ECG_HD uint32_t fold_windows() const { return tab ? 1u : W; }  // window sums per task
+  ECG_HD uint32_t digit_windows() const { return wd ? wd : W; }
 };
 
 // Task geometry.  A single MSM is one task (n_lines = n_chunks = 1).  The
@@ -326,7 +332,7 @@ ECG_DEV int32_t window_digit(const uint32_t* s, uint32_t w, const MsmPlan& pl, u
   }
   int32_t d = (int32_t)(v + carry);
   carry = 0;
-  if (w + 1 < pl.W && (uint32_t)d >= half) {
+  if (w + 1 < pl.digit_windows() && (uint32_t)d >= half) {
     d -= (int32_t)(1u << pl.c);
     carry = 1;
   }
@@ -376,8 +382,12 @@ __global__ void __launch_bounds__(MSM_THREADS)
   load_scalar<C>(scalars, j, g.scalar_mont, s);
   const uint32_t chunk = g.n_chunks == 1 ? 0u : (uint32_t)(j / g.clen);
   uint32_t carry = 0;
-  for (uint32_t w = 0; w < pl.W; w++) {
-    const int32_t d = window_digit(s, w, pl, carry);
+  const uint32_t wd = pl.digit_windows();
+  for (uint32_t wa = 0; wa < wd; wa++) {
+    const int32_t d = window_digit(s, wa, pl, carry);
+    if (wa < pl.w0) continue;  // a window piece emits windows [w0, w0 + W) only
+    const uint32_t w = wa - pl.w0;
+    if (w >= pl.W) break;
     const uint32_t mag = d < 0 ? (uint32_t)(-d) : (uint32_t)d;
     const uint32_t sign = d < 0 ? 0x80000000u : 0u;
     const size_t o = (size_t)w * mpad + j;
@@ -1671,7 +1681,49 @@ void msm_host_fold_bits(const XYZZ<typename C::Fq>* sums, const MsmPlan& e, host
     for (uint32_t k = 0; k < e.c; k++) acc = host::hjac_dbl(acc);
     acc = host::hjac_add(acc, host::hjac_from_xyzz(win[w]));
   }
+  // a window piece's first window is window w0 of the scalar: weight 2^(c w0)
+  for (uint32_t k = 0; k < e.c * e.w0; k++) acc = host::hjac_dbl(acc);
   total = host::hadd_pts(total, host::hxyzz_from_jac(acc));
+}
+
+// One piece of the (window x term) grid of an n_plan-term MSM: windows
+// [w0, w0 + nwin) of the n_plan-term plan over the m terms at d_bases /
+// d_scalars (views at the piece's first term).  Returns the piece's partial,
+// sum over its windows w and terms t of 2^(c w) d_w(s_t) P_t, normalised.
+// Every rank of ecg_msm_dist_grid runs its pieces with the same plan (from
+// n_plan), so the partials of all ranks add up to the whole MSM.
+template <class C>
+int msm_piece_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t m, size_t n_plan, uint32_t w0,
+                uint32_t nwin, uint64_t* out_jac, hipStream_t s, BaseForm bf) {
+  using HX = host::HPoint<HostF<C>>;
+  using X = XYZZ<typename C::Fq>;
+  if (bf.tab_c) {
+    set_error("multiexp: window pieces need plain prepared bases or [x, y] bases, not a window table");
+    return ECG_ERR_INVALID;
+  }
+  MsmPlan pl = make_plan(n_plan, (uint32_t)C::FrParams::BITS);
+  if (w0 + nwin > pl.W || nwin == 0 || m > 0x7fffffffull) {
+    set_error("multiexp: window piece [%u, %u) outside the %u windows of the plan", w0, w0 + nwin, pl.W);
+    return ECG_ERR_INVALID;
+  }
+  HX total = HX::zero();
+  if (m > 0) {
+    pl.wd = pl.W;
+    pl.w0 = w0;
+    pl.W = nwin;
+    pl.G = nwin;
+    plan_reduction(pl);  // the caller resets the msm_accumulate timer
+    const MsmGeom g{1, 1, m, m, 0};
+    void* d_sums;
+    ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums, bf.prepared));
+    const MsmPlan e = msm_eff_plan<C>(pl);
+    X* win;  // mapped pinned host memory (msm_sums_to_std_kernel)
+    ECG_TRY(hws_get(ctx, "msm_sums_host", msm_single_sums(e) * sizeof(X), (void**)&win));
+    ECG_HIP(hipStreamSynchronize(s));
+    msm_host_fold_bits<C>(win, e, total);
+  }
+  host::hto_jac_norm(total, out_jac);
+  return ECG_OK;
 }
 
 // Terms per device pass: calc_chunk_size (multiexp.rs:71-93) restated for

@@ -36,6 +36,7 @@ MsmOps ECG_OPS_NAME = {&msm_single_t<InstCurve>,        &batch_entry,
                        &msm_table_windows<InstCurve>,   &msm_table_auto<InstCurve>,
                        &point_sum_host_t<InstCurve>,    &gen_bases_t<InstCurve>,
                        &msm_pass_terms<InstCurve>,      &msm_host_t<InstCurve>,
-                       &msm_base_record_bytes<InstCurve>, &msm_plan_info_t<InstCurve>};
+                       &msm_base_record_bytes<InstCurve>, &msm_plan_info_t<InstCurve>,
+                       &msm_piece_t<InstCurve>};
 
 }  // namespace ecg

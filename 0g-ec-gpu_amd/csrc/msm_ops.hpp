@@ -25,6 +25,18 @@ struct MsmOps {
               uint64_t* out_jac, ecg_abort_cb, void* user, const MsmFill* fill);
   size_t (*record_bytes)();  // bytes per prepared base record (one table row)
   int (*plan_info)(size_t n, uint32_t window_bits, uint32_t* c, uint32_t* windows, int* sort_mode);
+  // windows [w0, w0 + nwin) of the n_plan-term plan over m terms (msm_piece_t)
+  int (*piece)(ecg_ctx*, const void* d_bases, const void* d_scalars, size_t m, size_t n_plan, uint32_t w0,
+               uint32_t nwin, uint64_t* out_jac, hipStream_t, BaseForm bf);
 };
+
+// This rank's share of an n-term MSM split over a grid of (window x term)
+// ranges (ecg_msm_dist_grid): the W windows of the n-term plan times the n
+// terms, in window-major order, cut into nranks equal contiguous ranges; rank
+// `rank` runs its range's pieces (a partial window, whole windows, a partial
+// window) over the full base and scalar arrays and returns their partial sum.
+// *pieces receives the number of pieces run.
+int msm_grid_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n, int rank,
+                 int nranks, uint64_t* out_jac, hipStream_t s, ecg_abort_cb abort_cb, void* user, int* pieces);
 
 }  // namespace ecg

@@ -136,6 +136,13 @@ _SIGS = {
                                     _u64p]),
     "ecg_msm_dist_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_size_t, _u64p, ABORT_CB, ctypes.c_void_p]),
+    "ecg_msm_dist_grid": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_size_t, _u64p]),
+    "ecg_msm_dist_grid_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_size_t, _u64p, ABORT_CB, ctypes.c_void_p]),
+    "ecg_msm_grid_part": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_size_t, ctypes.c_int, ctypes.c_int, _u64p,
+                                         ctypes.POINTER(ctypes.c_int)]),
     "ecg_fft_dist": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, _u64p, ctypes.c_uint32]),
     "ecg_fft_dist_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, _u64p, ctypes.c_uint32,
                                        ABORT_CB, ctypes.c_void_p]),
@@ -430,6 +437,19 @@ def msm_dev(prog: Program, curve, d_bases: DeviceBuffer, d_scalars: DeviceBuffer
     _check(lib().ecg_msm_dev(prog.handle, cid, d_bases.ptr, d_scalars.ptr, n,
                              out.ctypes.data_as(ctypes.c_void_p), 0, None), "msm_dev")
     return out
+
+
+def msm_grid_part(prog: Program, curve, d_bases: DeviceBuffer, d_scalars: DeviceBuffer, n: int, rank: int,
+                  nranks: int) -> tuple[np.ndarray, int]:
+    """Rank `rank` of `nranks`'s local step of the grid-split MSM
+    (ecg_msm_grid_part): its partial over the full n-term operands and the
+    number of Pippenger pieces it ran.  The nranks partials add up to msm_dev."""
+    cid = _curve(curve)
+    out = np.zeros(3 * CURVE_FQ_LIMBS[cid], dtype=np.uint64)
+    pieces = ctypes.c_int(0)
+    _check(lib().ecg_msm_grid_part(prog.handle, cid, d_bases.ptr, d_scalars.ptr, n, rank, nranks, _ptr(out),
+                                   ctypes.byref(pieces)), "msm_grid_part")
+    return out, pieces.value
 
 
 class PreparedBases(DeviceBuffer):

@@ -608,6 +608,24 @@ def msm_dist(prog, curve, d_bases, d_scalars, n_local: int, maybe_abort=None):
     return out
 
 
+def msm_dist_grid(prog, curve, d_bases, d_scalars, n: int, maybe_abort=None):
+    """Grid split (ecg_msm_dist_grid_ex): every rank passes ALL n bases and
+    scalars and runs 1/world of the n-term plan's (window x term) grid; the
+    [status | partial] records are exchanged and folded as in msm_dist."""
+    import numpy as np
+
+    import ecgpu
+
+    cid = ecgpu.CURVE_NAMES.get(curve, -1) if isinstance(curve, str) else int(curve)
+    out = np.zeros(3 * ecgpu.CURVE_FQ_LIMBS.get(cid, 12), dtype=np.uint64)
+    cb, keep = ecgpu._abort_cb(maybe_abort)
+    ecgpu._check(ecgpu.lib().ecg_msm_dist_grid_ex(prog.handle, cid, d_bases.ptr if d_bases is not None else None,
+                                                  d_scalars.ptr if d_scalars is not None else None, n,
+                                                  ecgpu._ptr(out), cb, None), "msm_dist_grid")
+    del keep
+    return out
+
+
 def fft_dist(prog, field, d_local, omega, log_n: int, maybe_abort=None) -> None:
     """One 2^log_n NTT, block-distributed over the communicator (in place);
     statuses exchanged before the first and the last all-to-all."""

@@ -128,6 +128,10 @@ def parse(argv=None):
                          "ranks on one GPU, which RCCL refuses)")
     ap.add_argument("--single-device", action="store_true",
                     help="every rank on GPU 0 (with --transport host: N-rank rehearsal on a one-GPU box)")
+    ap.add_argument("--msm-split", choices=("range", "grid"), default="range",
+                    help="N > 1 MSM split: 'range' = contiguous term shards (multiexp.rs:332-336, "
+                         "ecg_msm_dist); 'grid' = every rank holds all bases and scalars and runs 1/N of the "
+                         "(window x term) grid of the whole-n plan (ecg_msm_dist_grid, SURVEY §8(e))")
     ap.add_argument("--unprepared", action="store_true",
                     help="time the MSM over [x, y] bases (conversion to the kernel layout inside every step)")
     return ap.parse_args(argv)
@@ -239,7 +243,13 @@ def main():
 
     # ------------------------------------------------------------ MSM inputs (HBM-resident)
     n_total = 1 << args.msm_log
-    i0, n_loc, scal, a_loc = msm_shard(rank, world, n_total, r_int)
+    grid = world > 1 and args.msm_split == "grid"
+    all_shards = None
+    if grid:  # replicated operands: every rank holds all n_total bases and the scalars of every shard
+        all_shards = [msm_shard(r, world, n_total, r_int) for r in range(world)]
+        i0, n_loc, scal, a_loc = 0, n_total, np.concatenate([sh[2] for sh in all_shards]), KAT_A % r_int
+    else:
+        i0, n_loc, scal, a_loc = msm_shard(rank, world, n_total, r_int)
     d_scal = ecgpu.DeviceBuffer.upload(prog, scal)
     d_bases = ecgpu.gen_bases_dev(prog, args.curve, a_loc, KAT_B, n_loc)
     # upload_multiexp_bases (ag-cuda-ec/src/multiexp.rs:11-19): the resident
@@ -253,6 +263,8 @@ def main():
     def msm_step(bases=d_msm_bases):
         if world == 1:
             result[:] = ecgpu.msm_dev(prog, args.curve, bases, d_scal, n_loc)
+        elif grid:  # 1/N of the (window x term) grid + the same [status | partial] all-gather + fold
+            result[:] = edist.msm_dist_grid(prog, args.curve, bases, d_scal, n_total)
         else:  # local MSM + RCCL all-gather of world x 144 B partials + fold (no EC-add reduce op in RCCL)
             result[:] = edist.msm_dist(prog, args.curve, bases, d_scal, n_loc)
 
@@ -289,6 +301,8 @@ def main():
     barrier()
     msm_s = group.max(time.perf_counter() - t0) / args.steps
     acc_avg_ms = group.max(acc_ms / max(acc_launch, 1))
+    if grid:  # up to three pieces of different sizes per step: the roofline takes the per-step sum
+        acc_avg_ms = group.max(acc_ms / args.steps)
     if comm is not None:  # the last step's status + partial all-gather, slowest rank
         comm["msm_allgather_us"] = group.max(edist.last_exchange_us(prog))
     msm_result = result.copy()
@@ -308,7 +322,7 @@ def main():
     # the same MSM over a window table of the bases (fixed-base form, ecg_msm_prepare_table): reported
     # beside `value`, which stays on the per-call base layout the reference's API takes
     table = None
-    if not args.no_table and not args.unprepared and cid in (0, 1):
+    if not args.no_table and not args.unprepared and cid in (0, 1) and not grid:
         msm_prep = d_msm_bases
         t0 = time.perf_counter()
         d_tab = ecgpu.prepare_bases(prog, args.curve, d_bases, n_loc, window_table=0)
@@ -378,7 +392,7 @@ def main():
         import coracle as co
 
         # MSM known answer over all 2^26 terms (SURVEY §8c KAT), every rank's shard
-        shards = [(i0, n_loc, scal, a_loc)] if world == 1 else None
+        shards = [(i0, n_loc, scal, a_loc)] if world == 1 else all_shards
         kat = msm_kat_scalar(co, cid, world, n_total, r_int, nthreads, shards)
         want = co.jac_to_affine(cid, co.gen_mul(cid, kat))
         got = co.jac_to_affine(cid, msm_result)
@@ -701,7 +715,9 @@ def main():
         return
 
     # ------------------------------------------------------------ report
-    n_acc = n_loc  # terms per accumulation launch on rank 0 (the largest shard)
+    # terms per accumulation launch on rank 0 (the largest shard); grid split:
+    # a rank's W n / N grid cells per step count as n / N terms of W windows
+    n_acc = n_total // world if grid else n_loc
     W = -(-(r_int.bit_length() + 1) // 20) if args.msm_log >= 24 else None  # windows at c = 20
     bytes_per_term = 2 * lq * 8 + 32  # affine + 32 B scalar: 128 B (BLS12-381), 96 B (BN254), SURVEY §8(d)
     hbm_achieved = bytes_per_term * n_acc / (acc_avg_ms / 1e3) / 1e9
@@ -753,7 +769,9 @@ def main():
                    "(ecg_msm_prepare_bases, upload_multiexp_bases's role)"),
         "config": {"workload": f"{args.curve} G1 MSM 2^{args.msm_log} terms sharded over {world} GPU(s) "
                                f"+ Fr NTT 2^{log_n} per GPU", "msm_terms": n_total, "ntt_log_n": log_n,
-                   "parallelism": (f"range-shard x{world} + "
+                   "msm_split": args.msm_split if world > 1 else None,
+                   "parallelism": ((f"grid split (window x term) x{world}, replicated bases + " if grid
+                                    else f"range-shard x{world} + ")
                                    + ("RCCL" if args.transport == "rccl" else "host-group (rehearsal)")
                                    + " all-gather of partials") if world > 1 else "single GPU"},
         "msm_ms_unprepared_bases": unprep_ms,

@@ -384,6 +384,24 @@ int ecg_msm_dist(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_
  * every rank. */
 int ecg_msm_dist_ex(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n_local,
                     uint64_t *out_jac, ecg_abort_cb abort_cb, void *user);
+/* Grid split of the same MSM (SURVEY §8(e)'s window partitioning with
+ * replicated bases): every rank passes ALL n bases and scalars; the n-term
+ * plan's (window x term) grid is cut into nranks equal ranges of W n / nranks
+ * cells and rank r runs the r-th (a partial window, whole windows, a partial
+ * window: at most three Pippenger pieces, each with the whole-n plan's window
+ * width), so every rank does the same bucket work whatever n and nranks are.
+ * Partials and statuses are exchanged and folded as in ecg_msm_dist; the
+ * result is bit-identical to ecg_msm over the n terms.  Bases may be a
+ * prepared buffer (ecg_msm_prepare) or [x, y] records, not a window table. */
+int ecg_msm_dist_grid(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n,
+                      uint64_t *out_jac);
+int ecg_msm_dist_grid_ex(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n,
+                         uint64_t *out_jac, ecg_abort_cb abort_cb, void *user);
+/* Rank `rank` of `nranks`'s local step of ecg_msm_dist_grid on this context,
+ * without an exchange: its partial (normalised Jacobian) in out_jac and, if
+ * pieces is not NULL, the number of Pippenger pieces it ran. */
+int ecg_msm_grid_part(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n, int rank,
+                      int nranks, uint64_t *out_jac, int *pieces);
 /* One NTT of 2^log_n points, block-distributed (rank r holds points
  * [r m, (r+1) m), m = 2^log_n / nranks), in place, natural order: the
  * four-step split of parallel_fft (fft_cpu.rs:59-111) with three RCCL

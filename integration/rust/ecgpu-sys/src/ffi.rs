@@ -166,6 +166,13 @@ extern "C" {
                         n_local: usize, out_jac: *mut u64) -> c_int;
     pub fn ecg_msm_dist_ex(ctx: *mut ecg_ctx, curve_id: c_int, d_bases: *const c_void, d_scalars: *const c_void,
                            n_local: usize, out_jac: *mut u64, abort_cb: ecg_abort_cb, user: *mut c_void) -> c_int;
+    pub fn ecg_msm_dist_grid(ctx: *mut ecg_ctx, curve_id: c_int, d_bases: *const c_void, d_scalars: *const c_void,
+                             n: usize, out_jac: *mut u64) -> c_int;
+    pub fn ecg_msm_dist_grid_ex(ctx: *mut ecg_ctx, curve_id: c_int, d_bases: *const c_void,
+                                d_scalars: *const c_void, n: usize, out_jac: *mut u64, abort_cb: ecg_abort_cb,
+                                user: *mut c_void) -> c_int;
+    pub fn ecg_msm_grid_part(ctx: *mut ecg_ctx, curve_id: c_int, d_bases: *const c_void, d_scalars: *const c_void,
+                             n: usize, rank: c_int, nranks: c_int, out_jac: *mut u64, pieces: *mut c_int) -> c_int;
     pub fn ecg_fft_dist(ctx: *mut ecg_ctx, field_id: c_int, d_local: *mut c_void, omega: *const u64,
                         log_n: u32) -> c_int;
     pub fn ecg_fft_dist_ex(ctx: *mut ecg_ctx, field_id: c_int, d_local: *mut c_void, omega: *const u64,

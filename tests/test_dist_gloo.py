@@ -170,6 +170,16 @@ def _install_device_fakes(rank, world, corrupt=False, fail_rank=None):
                 raise ecgpu.EcError(f"msm_dist: ecg_msm_dist: rank {r} of {world} failed (rc={rc}); every rank stops")
         return _fold(co, cid, [p for _, p in recs])
 
+    def msm_dist_grid(prog, curve, bases, scal, n, maybe_abort=None):
+        # every rank holds all n terms; this stand-in's "1/N of the grid" is a
+        # term range of them (the partials fold to the same total)
+        cid = ecgpu._curve(curve)
+        nq = ecgpu.CURVE_FQ_LIMBS[cid]
+        assert bases.arr.size == n * 2 * nq and scal.arr.size == n * 4, "grid split needs replicated operands"
+        i0, i1 = edist.shard_range(n, world, rank)
+        sub_b, sub_s = _FakeBuf(bases.arr.reshape(-1, 2 * nq)[i0:i1]), _FakeBuf(scal.arr.reshape(-1, 4)[i0:i1])
+        return msm_dist(prog, curve, sub_b, sub_s, i1 - i0, maybe_abort)
+
     def fft_dev(prog, field, d, omega, log_n):
         d.arr[...] = co.serial_fft(fid_of[field], d.arr.reshape(-1, 4), np.asarray(omega, np.uint64), log_n)
 
@@ -192,6 +202,7 @@ def _install_device_fakes(rank, world, corrupt=False, fail_rank=None):
     edist.comm_init = lambda prog, r, w, bcast, **kw: real_comm_init(None, r, w, bcast,
                                                                      make_id=lambda: bytes(range(128)))
     edist.msm_dist = msm_dist
+    edist.msm_dist_grid = msm_dist_grid
     edist.fft_dist = fft_dist
     # what an RCCL communicator of `world` ranks on distinct devices reports
     edist.comm_info = lambda prog: {"count": world, "rank": rank, "device": rank,
@@ -200,7 +211,7 @@ def _install_device_fakes(rank, world, corrupt=False, fail_rank=None):
     return side
 
 
-def _bench_main_worker(rank, world, port, q, corrupt=False, fail_rank=None):
+def _bench_main_worker(rank, world, port, q, corrupt=False, fail_rank=None, extra=()):
     import contextlib
     import io
 
@@ -215,7 +226,7 @@ def _bench_main_worker(rank, world, port, q, corrupt=False, fail_rank=None):
     import ecgpu
 
     sys.argv = ["bench.py", "--gpus", str(world), "--steps", "2", "--warmup", "1", "--msm-log", "10",
-                "--ntt-log", "8"]
+                "--ntt-log", "8", *extra]
     out = io.StringIO()
     try:
         with contextlib.redirect_stdout(out):
@@ -259,6 +270,30 @@ def test_bench_main_world2(corrupt):
     assert line["rccl"] == {"transport": ["rccl"], "count": [2], "ranks": [0, 1],
                             "devices": ["0000:11:00.0", "0000:21:00.0"], "distinct": True,
                             "msm_allgather_us": 41.0}
+
+
+@pytest.mark.timeout(300)
+def test_bench_main_world2_grid_split():
+    """bench.main() at N = 2 with --msm-split grid: every rank generates all
+    2^10 bases and the scalars of both shards, the JSON line records the split
+    and the full-size KAT holds."""
+    import multiprocessing as mp
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_main_worker, args=(r, 2, port, q, False, None, ("--msm-split", "grid")))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    outs = dict(q.get(timeout=10) for _ in range(2))
+    assert all(p.exitcode == 0 for p in procs)
+    line = json.loads(outs[0].strip().splitlines()[-1])
+    assert line["config"]["msm_split"] == "grid" and "grid split" in line["config"]["parallelism"]
+    assert line["checks"]["msm_kat_2^10"] is True
+    assert line["msm_window_table"] is None
 
 
 @pytest.mark.timeout(300)

@@ -412,3 +412,129 @@ def test_config4_msm_2p26_eight_shards(gpu_programs, cname, cid):
             p.close()
         prep.free()
         d_sc.free()
+
+
+def _fold_parts(cid, parts):
+    nq = ecgpu.CURVE_FQ_LIMBS[cid]
+    acc = np.zeros(3 * nq, dtype=np.uint64)
+    for p in parts:
+        p = np.ascontiguousarray(p, dtype=np.uint64)
+        co.lib().orc_jac_add(cid, co.ptr(acc), co.ptr(acc), co.ptr(p))
+    return acc
+
+
+@pytest.mark.parametrize("cname,cid", [("bls12_381", 0), ("bn254", 1)])
+@pytest.mark.parametrize("prepared", [False, True])
+def test_msm_grid_parts(gpu_programs, cname, cid, prepared):
+    """Grid split's per-rank step (ecg_msm_grid_part): for rank counts that
+    cut windows mid-way (3, 5, 13), exactly on window edges (1, 2, 8) and
+    more ranks than grid cells (n = 1), the nranks partials fold to
+    multiexp_cpu of the whole input, bit-exact, and no rank runs more than
+    three Pippenger pieces (partial window, whole windows, partial window)."""
+    prog = gpu_programs[0][0]
+    cv = po.CURVES[cname]
+    for n, seed in ((5003, 3), (7, 4), (1, 5)):
+        B = co.gen_bases(cid, 23, 29, n, 8)
+        E = rand_fr(cv.fr, n, seed + 20 * cid)
+        want = co.jac_to_affine(cid, co.multiexp_cpu(cid, B, E, nthreads=8))
+        d_b = ecgpu.DeviceBuffer.upload(prog, B)
+        d_e = ecgpu.DeviceBuffer.upload(prog, E)
+        bases = ecgpu.prepare_bases(prog, cname, d_b, n) if prepared else d_b
+        try:
+            for nranks in (1, 2, 3, 5, 8, 13):
+                parts, pieces = [], []
+                for r in range(nranks):
+                    p, k = ecgpu.msm_grid_part(prog, cname, bases, d_e, n, r, nranks)
+                    parts.append(p)
+                    pieces.append(k)
+                assert max(pieces) <= 3, (n, nranks, pieces)
+                got = co.jac_to_affine(cid, _fold_parts(cid, parts))
+                assert (got == want).all(), (n, nranks)
+        finally:
+            if prepared:
+                bases.free()
+            d_b.free()
+            d_e.free()
+
+
+def test_msm_grid_part_rejects(gpu_programs):
+    """Bad rank numbers and window-table bases are refused, not run."""
+    prog = gpu_programs[0][0]
+    n = 64
+    B = co.gen_bases(0, 3, 5, n, 2)
+    E = rand_fr(po.CURVES["bls12_381"].fr, n, 1)
+    d_b = ecgpu.DeviceBuffer.upload(prog, B)
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    try:
+        for r, nr in ((2, 2), (-1, 2), (0, 0)):
+            with pytest.raises(ecgpu.EcError):
+                ecgpu.msm_grid_part(prog, "bls12_381", d_b, d_e, n, r, nr)
+        tab = ecgpu.prepare_bases(prog, "bls12_381", d_b, n, window_table=8)
+        try:
+            with pytest.raises(ecgpu.EcError, match="window table"):
+                ecgpu.msm_grid_part(prog, "bls12_381", tab, d_e, n, 0, 2)
+        finally:
+            tab.free()
+    finally:
+        d_b.free()
+        d_e.free()
+
+
+@pytest.mark.parametrize("cname,cid", [("bls12_381", 0), ("bn254", 1)])
+@pytest.mark.parametrize("world", [2, 3])
+def test_msm_dist_grid_host_transport(gpu_programs, cname, cid, world):
+    """ecg_msm_dist_grid with `world` ranks on one GPU (host transport),
+    every rank holding all bases and scalars: every rank returns multiexp_cpu
+    of the whole input, bit-exact."""
+    progs = _host_ranks(gpu_programs[1][0], world)
+    try:
+        cv = po.CURVES[cname]
+        n = 4099
+        B = co.gen_bases(cid, 31, 37, n, 8)
+        E = rand_fr(cv.fr, n, 40 + world + cid)
+        want = co.jac_to_affine(cid, co.multiexp_cpu(cid, B, E, nthreads=8))
+        d_b = [ecgpu.DeviceBuffer.upload(p, B) for p in progs]
+        d_e = [ecgpu.DeviceBuffer.upload(p, E) for p in progs]
+        res = _run_ranks(world, lambda r: edist.msm_dist_grid(progs[r], cname, d_b[r], d_e[r], n))
+        for ok, got in res:
+            assert ok, got
+            assert (co.jac_to_affine(cid, got) == want).all()
+        for b in d_b + d_e:
+            b.free()
+    finally:
+        for p in progs:
+            p.close()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("cname,cid", [("bls12_381", 0), ("bn254", 1)])
+def test_config4_msm_2p26_grid_split(gpu_programs, cname, cid):
+    """BASELINE config 4 through the grid split: 2^26 bases prepared once and
+    the 2^26 scalars bench.py generates (all shards concatenated) are shared by
+    8 host-transport ranks, each running 1/8 of the (window x term) grid of
+    the 2^26 plan; every rank returns the 2^26 known answer."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    world, n_total = 8, 1 << 26
+    r_int = bench.R_BLS if cid == 0 else bench.R_BN
+    prog0 = gpu_programs[0][0]
+    d_raw = ecgpu.gen_bases_dev(prog0, cname, bench.KAT_A % r_int, bench.KAT_B, n_total)
+    prep = ecgpu.prepare_bases(prog0, cname, d_raw, n_total)
+    d_raw.free()
+    shards = [bench.msm_shard(r, world, n_total, r_int) for r in range(world)]
+    d_sc = ecgpu.DeviceBuffer.upload(prog0, np.concatenate([s[2] for s in shards]))
+    progs = _host_ranks(gpu_programs[1][0], world, timeout_s=300)
+    try:
+        res = _run_ranks(world, lambda r: edist.msm_dist_grid(progs[r], cname, prep, d_sc, n_total))
+        assert all(ok for ok, _ in res), res
+        first = res[0][1]
+        assert all((v == first).all() for _, v in res)
+        kat = bench.msm_kat_scalar(co, cid, world, n_total, r_int, 16, shards)
+        want = co.jac_to_affine(cid, co.gen_mul(cid, kat))
+        assert (co.jac_to_affine(cid, first) == want).all()
+    finally:
+        for p in progs:
+            p.close()
+        prep.free()
+        d_sc.free()
