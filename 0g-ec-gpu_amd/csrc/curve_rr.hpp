@@ -596,6 +596,15 @@ template <>
 struct RR1of<params::bn254_fq> {
   using Q = params::bn254_fq9_rr;
 };
+// BLS12-381 G1 buckets: 13 x 30 bits (338 instead of 392 mads per product,
+// split columns, tight-slack formulas at R'/p ~ 2^9.4); A/B: -DECG_BLS_FQ14
+// keeps 14 x 29 bits
+#ifndef ECG_BLS_FQ14
+template <>
+struct RR1of<params::bls12_381_fq> {
+  using Q = params::bls12_381_fq13_rr;
+};
+#endif
 template <class C>
 constexpr bool has_rr_form() {
   return C::EXT == 1 && !std::is_same<typename RRof<typename C::FqParams>::Q, void>::value;
@@ -609,7 +618,10 @@ ECG_DEV F pa_neg_y(const F& y) {
 }
 template <class Q>
 ECG_DEV FpR<Q> pa_neg_y(const FpR<Q>& y) {
-  return rr_neg_wide<4>(y);
+  if constexpr (Q::BITS > 29)  // 30-bit limbs: wide limbs (< 3 2^30) would overflow the product columns
+    return rr_neg<4>(y);
+  else
+    return rr_neg_wide<4>(y);
 }
 
 // k P for a small unsigned k (double-and-add from the MSB)

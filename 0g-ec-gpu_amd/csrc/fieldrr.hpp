@@ -103,6 +103,48 @@ ECG_DEV void rr_ceil_step(uint64_t& z, uint32_t& m, bool last) {
   if (last) z += 1;
 }
 
+// Column splits (BITS = 30: BLS12-381's 13 x 30-bit G1 layout).  A product
+// of two QN limbs (<= 2^30 + 3) is just above 2^60, so a 64-bit column holds
+// about 15 of them.  The m p products of a column are bounded by the modulus
+// limbs themselves (sum of (2^30 - 1) P_j over the column's j, at most 6.7
+// x 2^60 for all 13 limbs), so only the columns whose bound below -- `sets`
+// NL-product sets of QN limbs (a b; a b + c d in rr_mul_sum2), the m p terms
+// and a 2^37 carry-in -- reaches 2^64 are split (columns 10-14 of a 13-limb
+// product): after the a b products the accumulator keeps its low BITS bits
+// and the rest (h, a multiple of 2^BITS) skips the m p products and rejoins
+// the carry-out.  A squaring's doubled off-diagonal product counts twice, so
+// its columns bound like a product's.  BITS <= 29 never splits (2 NL
+// products of 2^58 fit).
+template <class Q>
+constexpr int rr_col_half(int k) {  // a b (or m p) products in column k
+  return k < Q::NL ? k + 1 : 2 * Q::NL - 1 - k;
+}
+template <class Q>
+constexpr bool rr_col_fits(int k, int sets) {
+  using u128 = unsigned __int128;
+  const u128 lim = (u128)1 << Q::BITS, qn = lim + 3;
+  u128 s = (u128)sets * (u128)rr_col_half<Q>(k) * qn * qn + ((u128)1 << 37);
+  const int j0 = k < Q::NL ? 0 : k - Q::NL + 1, j1 = k < Q::NL ? k : Q::NL - 1;
+  for (int j = j0; j <= j1; j++) s += (lim - 1) * (u128)Q::P[j];
+  return s < ((u128)1 << 64);
+}
+template <class Q>
+constexpr bool rr_col_split(int k, int sets = 1) {
+  return Q::BITS > 29 && !rr_col_fits<Q>(k, sets);
+}
+// (Keeping the low 32 bits instead -- h = the high word, no shift -- costs
+// more: the zeroed high word and the joined h need 64-bit moves.)
+template <class Q>
+ECG_DEV void rr_split(uint64_t& x, uint64_t& h) {
+  static_assert(Q::BITS <= 29 || !rr_ceil_carry<Q>(), "the ceil-carry chains (signed z) are not split");
+  h = x >> Q::BITS;
+  x &= (uint64_t)((1u << Q::BITS) - 1);
+}
+template <class Q>
+ECG_DEV void rr_join(uint64_t& x, uint64_t h) {
+  x += h;
+}
+
 // Montgomery product (a b + m p) / R', product scanning, one v_mad_u64_u32
 // per product.
 template <class Q>
@@ -116,6 +158,8 @@ ECG_DEV FpR<Q> rr_mul(const FpR<Q>& a, const FpR<Q>& b) {
   for (int k = 0; k < NL; k++) {
 #pragma unroll
     for (int i = 0; i <= k; i++) mad64(acc, a.v[i], b.v[k - i]);
+    uint64_t h = 0;
+    if (rr_col_split<Q>(k)) rr_split<Q>(acc, h);
 #pragma unroll
     for (int i = 0; i < k; i++) mad64s(acc, m[i], Q::P[k - i]);
     if constexpr (rr_ceil_carry<Q>()) {
@@ -124,16 +168,20 @@ ECG_DEV FpR<Q> rr_mul(const FpR<Q>& a, const FpR<Q>& b) {
       m[k] = ((uint32_t)acc * Q::INV) & MASK;
       mad64s(acc, m[k], Q::P[0]);  // low BITS bits of acc become 0
       acc >>= B;
+      if (rr_col_split<Q>(k)) rr_join<Q>(acc, h);
     }
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
 #pragma unroll
     for (int i = k - NL + 1; i < NL; i++) mad64(acc, a.v[i], b.v[k - i]);
+    uint64_t h = 0;
+    if (rr_col_split<Q>(k)) rr_split<Q>(acc, h);
 #pragma unroll
     for (int i = k - NL + 1; i < NL; i++) mad64s(acc, m[i], Q::P[k - i]);
     r.v[k - NL] = (uint32_t)acc & MASK;
     acc >>= B;
+    if (rr_col_split<Q>(k)) rr_join<Q>(acc, h);
   }
   r.v[NL - 1] = (uint32_t)acc;
   return r;
@@ -352,6 +400,11 @@ ECG_DEV void rr_mul2(const FpR<Q>& a0, const FpR<Q>& b0, const FpR<Q>& a1, const
 #pragma unroll
   for (int k = 0; k < NL; k++) {
     if (k > 0) col2(k, 0, k, x0, a0.v, b0.v, x1, a1.v, b1.v);
+    uint64_t h0 = 0, h1 = 0;
+    if (rr_col_split<Q>(k)) {
+      rr_split<Q>(x0, h0);
+      rr_split<Q>(x1, h1);
+    }
     col2p<Q>(k, 0, k - 1, x0, m0, x1, m1);
     if constexpr (rr_ceil_carry<Q>()) {
       rr_ceil_step<Q>(x0, m0[k], k == NL - 1);
@@ -362,16 +415,29 @@ ECG_DEV void rr_mul2(const FpR<Q>& a0, const FpR<Q>& b0, const FpR<Q>& a1, const
       mad64x2s(x0, m0[k], x1, m1[k], Q::P[0]);
       x0 >>= B;
       x1 >>= B;
+      if (rr_col_split<Q>(k)) {
+        rr_join<Q>(x0, h0);
+        rr_join<Q>(x1, h1);
+      }
     }
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; k++) {
     col2(k, k - NL + 1, NL - 1, x0, a0.v, b0.v, x1, a1.v, b1.v);
+    uint64_t h0 = 0, h1 = 0;
+    if (rr_col_split<Q>(k)) {
+      rr_split<Q>(x0, h0);
+      rr_split<Q>(x1, h1);
+    }
     col2p<Q>(k, k - NL + 1, NL - 1, x0, m0, x1, m1);
     r0.v[k - NL] = (uint32_t)x0 & MASK;
     r1.v[k - NL] = (uint32_t)x1 & MASK;
     x0 >>= B;
     x1 >>= B;
+    if (rr_col_split<Q>(k)) {
+      rr_join<Q>(x0, h0);
+      rr_join<Q>(x1, h1);
+    }
   }
   r0.v[NL - 1] = (uint32_t)x0;
   r1.v[NL - 1] = (uint32_t)x1;
@@ -405,6 +471,18 @@ ECG_DEV FpR<Q> rr_mul_sum2(const FpR<Q>& a, const FpR<Q>& b, const FpR<Q>& c, co
       mad64x2_z<true, true>(x0, a.v[0], b.v[0], x1, c.v[0], d.v[0]);
     else  // chain 1 restarts at zero in every column
       col2<true>(k, i0, i1, x0, a.v, b.v, x1, c.v, d.v);
+    // BITS = 30: three product sets per column -- split both chains after
+    // a b | c d and restart chain 1 for its half of the m p products
+    const bool sp = rr_col_split<Q>(k, 2);
+    uint64_t h = 0;
+    if (sp) {
+      uint64_t h1;
+      rr_split<Q>(x0, h);
+      rr_split<Q>(x1, h1);
+      h += h1;
+      x0 += x1;
+      x1 = 0;
+    }
     const int j1 = k < NL ? k - 1 : NL - 1;  // m[j] p[k-j], j in [i0, j1]
     int j = i0;
 #pragma unroll
@@ -418,6 +496,7 @@ ECG_DEV FpR<Q> rr_mul_sum2(const FpR<Q>& a, const FpR<Q>& b, const FpR<Q>& c, co
       r.v[k - NL] = (uint32_t)x0 & MASK;
     }
     x0 >>= B;
+    if (sp) rr_join<Q>(x0, h);
   }
   r.v[NL - 1] = (uint32_t)x0;
   return r;
@@ -443,6 +522,11 @@ ECG_DEV void rr_sqr2(const FpR<Q>& a0, const FpR<Q>& a1, FpR<Q>& r0, FpR<Q>& r1)
       mad64x2_z<true, true>(x0, a0.v[0], a0.v[0], x1, a1.v[0], a1.v[0]);
     else if ((k & 1) == 0)
       mad64x2(x0, a0.v[k >> 1], a0.v[k >> 1], x1, a1.v[k >> 1], a1.v[k >> 1]);
+    uint64_t h0 = 0, h1 = 0;
+    if (rr_col_split<Q>(k)) {
+      rr_split<Q>(x0, h0);
+      rr_split<Q>(x1, h1);
+    }
     if (k < NL) {
       col2p<Q>(k, 0, k - 1, x0, m0, x1, m1);
       m0[k] = ((uint32_t)x0 * Q::INV) & MASK;
@@ -455,6 +539,10 @@ ECG_DEV void rr_sqr2(const FpR<Q>& a0, const FpR<Q>& a1, FpR<Q>& r0, FpR<Q>& r1)
     }
     x0 >>= B;
     x1 >>= B;
+    if (rr_col_split<Q>(k)) {
+      rr_join<Q>(x0, h0);
+      rr_join<Q>(x1, h1);
+    }
   }
   r0.v[NL - 1] = (uint32_t)x0;
   r1.v[NL - 1] = (uint32_t)x1;
@@ -477,6 +565,8 @@ ECG_DEV FpR<Q> rr_sqr(const FpR<Q>& a) {
 #pragma unroll
     for (int i = i0; 2 * i < k; i++) mad64(acc, a2[i], a.v[k - i]);
     if ((k & 1) == 0) mad64(acc, a.v[k >> 1], a.v[k >> 1]);
+    uint64_t h = 0;
+    if (rr_col_split<Q>(k)) rr_split<Q>(acc, h);
     if (k < NL) {
 #pragma unroll
       for (int i = 0; i < k; i++) mad64s(acc, m[i], Q::P[k - i]);
@@ -488,6 +578,7 @@ ECG_DEV FpR<Q> rr_sqr(const FpR<Q>& a) {
       r.v[k - NL] = (uint32_t)acc & MASK;
     }
     acc >>= B;
+    if (rr_col_split<Q>(k)) rr_join<Q>(acc, h);
   }
   r.v[NL - 1] = (uint32_t)acc;
   return r;
@@ -548,7 +639,10 @@ ECG_DEV FpR<Q> rr_neg(const FpR<Q>& a) {
 template <int K, class Q>
 ECG_DEV FpR<Q> rr_sub3(const FpR<Q>& a, const FpR<Q>& b, const FpR<Q>& c, const FpR<Q>& d) {
   constexpr int j = kp_index<K>();
-  static_assert((Q::KPD_OK >> j) & 1, "K p (deep borrow) not representable for this field");
+  if constexpr (Q::BITS > 29) {  // no deep borrow in 32-bit limbs: sum the subtrahends first
+    return rr_sub<K>(a, rr_add(b, rr_add(c, d)));
+  }
+  static_assert(Q::BITS > 29 || ((Q::KPD_OK >> j) & 1), "K p (deep borrow) not representable for this field");
   uint32_t s[Q::NL];
 #pragma unroll
   for (int i = 0; i < Q::NL; i++) s[i] = a.v[i] + Q::KPD[j][i] - b.v[i] - c.v[i] - d.v[i];
@@ -559,7 +653,10 @@ ECG_DEV FpR<Q> rr_sub3(const FpR<Q>& a, const FpR<Q>& b, const FpR<Q>& c, const 
 template <int K, class Q>
 ECG_DEV FpR<Q> rr_sub2(const FpR<Q>& a, const FpR<Q>& b, const FpR<Q>& c) {
   constexpr int j = kp_index<K>();
-  static_assert((Q::KPD_OK >> j) & 1, "K p (deep borrow) not representable for this field");
+  if constexpr (Q::BITS > 29) {
+    return rr_sub<K>(a, rr_add(b, c));
+  }
+  static_assert(Q::BITS > 29 || ((Q::KPD_OK >> j) & 1), "K p (deep borrow) not representable for this field");
   uint32_t s[Q::NL];
 #pragma unroll
   for (int i = 0; i < Q::NL; i++) s[i] = a.v[i] + Q::KPD[j][i] - b.v[i] - c.v[i];
