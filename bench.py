@@ -63,10 +63,10 @@ MSM_SEED = 0x35A00026
 NTT_SEED = 0x0FF70024
 KAT_A = 0x1234567890ABCDEF1122334455667788
 KAT_B = 0x0FEDCBA987654321
-# reduced-radix limbs of the MSM's G1 Fq (fieldrr.hpp): 14 x 29 bits (BLS12-381), 9 x 29 (BN254,
-# the tight-slack layout bn254_fq9_rr)
-RR_LIMBS = {0: 14, 1: 9}
-RR_BITS = {0: 29, 1: 29}
+# reduced-radix limbs of the MSM's G1 Fq (fieldrr.hpp): 13 x 30 bits (BLS12-381, bls12_381_fq13_rr,
+# split columns), 9 x 29 (BN254, bn254_fq9_rr); both tight-slack layouts (curve_rr.hpp)
+RR_LIMBS = {0: 13, 1: 9}
+RR_BITS = {0: 30, 1: 29}
 # v_mad_u64_u32 per reduced-radix Fr product as ntt.hip executes it (9 x 29-bit limbs: 81 schoolbook +
 # 81 reduction mads; BLS12-381's r = 1 mod 2^32 drops the m*P[0] mad of each of the 9 reduction columns
 # in the ceil-carry form, fieldrr.hpp rr_ceil_carry)
@@ -77,8 +77,9 @@ def madd_mads(nl: int) -> int:
     """v_mad_u64_u32 per XYZZ mixed add (rr_add_affine, curve_rr.hpp): three
     paired products (2 NL^2 each: schoolbook + Montgomery reduction) x 2, one
     paired squaring (NL(NL+1)/2 + NL^2) x 2, one product sum with a shared
-    reduction (3 NL^2).  3542 for BLS12-381 (matches SQ_INSTS_VALU_INT64 per
-    add, profiles/r02)."""
+    reduction (3 NL^2).  3055 for BLS12-381's 13 limbs (3542 with 14), 1467
+    for BN254's 9 -- the main block's static count (tools/isa_count.py,
+    profiles/r05/isa_accumulate_fq13.txt)."""
     mul, sqr = 2 * nl * nl, nl * (nl + 1) // 2 + nl * nl
     return 6 * mul + 2 * sqr + 3 * nl * nl
 
