@@ -142,6 +142,64 @@ static hipError_t msm_sort(int cfg, void* tmp, size_t& bytes, const uint64_t* ei
 }
 ECG_HD uint64_t msm_entry(uint32_t key, uint32_t val) { return ((uint64_t)key << 32) | val; }
 
+// The headline blocks' sort (c = 20, one block of < 2^32 entries per window)
+// without onesweep's histogram pass: the two 10-bit places' global digit
+// offsets -- offs[0, 1024) for key bits [0, 10), offs[1024, 2048) for [10,
+// 20), exclusive scans of the digit counts -- come from the digits kernel
+// (msm_digits_hist_kernel, msm_hist_scan_kernel), which counts every entry
+// as it writes it; this driver runs rocPRIM's two onesweep iterations (the
+// decoupled look-back scatter passes of SortCfg10b) on them, as
+// radix_sort_onesweep_impl does after its own histogram and scan kernels.
+// A rocPRIM-internal entry point (rocprim::detail, the ROCm install's
+// headers): msm_sort stays the fallback and the A/B (ECG_MSM_FUSED_HIST=0).
+static hipError_t msm_sort_fused(void* tmp, size_t& bytes, const uint64_t* ei, uint64_t* eo, unsigned int n,
+                                 unsigned int* offs, hipStream_t s) {
+  namespace rd = rocprim::detail;
+  using Cfg = typename SortCfg10b::onesweep_config;
+  using WCfg = rd::wrapped_radix_sort_onesweep_config<Cfg, uint64_t, rocprim::empty_type>;
+  bool use_atomic = false;
+  ROCPRIM_RETURN_ON_ERROR(rd::check_if_using_atomic_block_id(s, use_atomic));
+  rd::target_arch arch;
+  ROCPRIM_RETURN_ON_ERROR(rd::host_target_arch(s, arch));
+  const rd::radix_sort_onesweep_config_params params = rd::dispatch_target_arch<WCfg, false>(arch);
+  if (params.radix_bits_per_place != 10) return hipErrorInvalidValue;  // offs holds two 10-bit places
+  const unsigned int per_block = params.sort.block_size * params.sort.items_per_thread;
+  const unsigned int nlook = 1024u * ((n + per_block - 1) / per_block);
+  auto run = [&](auto atomic_id) -> hipError_t {
+    using Bid = rd::block_id_wrapper<unsigned int, decltype(atomic_id)::value>;
+    unsigned int* offs_tmp;
+    rd::onesweep_lookback_state* look;
+    uint64_t* keys_tmp;
+    typename Bid::id_type* bid_store;
+    ROCPRIM_RETURN_ON_ERROR(rd::temp_storage::partition(
+        tmp, bytes,
+        rd::temp_storage::make_linear_partition(rd::temp_storage::ptr_aligned_array(&offs_tmp, 1024u),
+                                                rd::temp_storage::ptr_aligned_array(&look, nlook),
+                                                rd::temp_storage::ptr_aligned_array(&keys_tmp, n),
+                                                rd::temp_storage::make_partition(&bid_store,
+                                                                                 Bid::get_temp_storage_layout()))));
+    if (tmp == nullptr || n == 0) return hipSuccess;
+    Bid bid = Bid::create(bid_store);
+    rocprim::empty_type* nv = nullptr;
+    ROCPRIM_RETURN_ON_ERROR((rd::radix_sort_onesweep_iteration<Cfg, false>(
+        ei, keys_tmp, eo, nv, nv, nv, n, offs, offs_tmp, look, true, false, rocprim::identity_decomposer{}, 32u, 52u,
+        bid, s, false)));
+    return rd::radix_sort_onesweep_iteration<Cfg, false>(ei, keys_tmp, eo, nv, nv, nv, n, offs + 1024, offs_tmp,
+                                                         look, false, true, rocprim::identity_decomposer{}, 42u,
+                                                         52u, bid, s, false);
+  };
+  return use_atomic ? run(std::true_type{}) : run(std::false_type{});
+}
+// A/B switch, off by default: ECG_MSM_FUSED_HIST=1 counts the digits in the
+// digits kernel.  Measured a wash at 2^24 and 2^26 (profiles/r05/fused_hist_ab.log):
+// the 13 histogram launches go (1.9 ms) but the digits kernel's LDS atomics
+// cost as much (1.54 -> 3.4 ms) -- rocPRIM's histogram pass is bound by the
+// same LDS atomics, not by re-reading the entries.
+static bool msm_fused_hist_enabled() {
+  static const bool v = env_u32("ECG_MSM_FUSED_HIST", 0) != 0;
+  return v;
+}
+
 struct MsmPlan {
   uint32_t c;     // window bits
   uint32_t W;     // windows
@@ -364,17 +422,25 @@ struct KeyMap {
 // key = (chunk(j) * W + w, |d| - 1) and value = j | sign, and the
 // accumulation walks the sorted list once per line (base and bucket offsets
 // per line).
-template <class C>
-__global__ void __launch_bounds__(MSM_THREADS)
-    msm_digits_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, size_t mpad, KeyMap km,
-                      uint64_t* __restrict__ ents) {
+// The entries of scalar j (j < mpad); HIST: each entry's 20-bit local key also
+// counts in the per-window digit histograms hist[(w 2 + place) 1024 + digit]
+// (LDS, msm_digits_hist_kernel; window-padded keys with c = 20 only).
+template <class C, bool HIST>
+ECG_DEV void msm_digits_one(const uint4* __restrict__ scalars, const MsmGeom& g, const MsmPlan& pl, size_t mpad,
+                            const KeyMap& km, uint64_t* __restrict__ ents, size_t j, uint32_t* hist) {
   const size_t m = (size_t)g.n_chunks * g.clen;
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= mpad) return;
+  auto count = [&](uint32_t w, uint32_t local) {  // 16-bit counters, two per LDS word
+    if constexpr (HIST) {
+      const uint32_t b0 = (w * 2) * 1024 + (local & 1023u), b1 = (w * 2 + 1) * 1024 + (local >> 10);
+      atomicAdd(&hist[b0 >> 1], 1u << ((b0 & 1) * 16));
+      atomicAdd(&hist[b1 >> 1], 1u << ((b1 & 1) * 16));
+    }
+  };
   if (j >= m) {  // block padding (window-padded mode only): block sentinels
     for (uint32_t w = 0; w < pl.W; w++) {
       const size_t o = (size_t)w * mpad + j;
       ents[o] = msm_entry((w << km.kc) | km.B, 0);
+      count(w, km.B);
     }
     return;
   }
@@ -395,11 +461,72 @@ __global__ void __launch_bounds__(MSM_THREADS)
     // of base j, record j * W + w (the rows of a base sit together)
     const uint32_t grp = pl.tab ? chunk : chunk * pl.W + w;
     const uint32_t bidx = pl.tab ? (uint32_t)j * pl.W + w : (uint32_t)j;
-    if (d == 0)
+    if (d == 0) {
       ents[o] = msm_entry(km.kc ? (grp << km.kc) | km.B : km.sentinel, 0);
-    else
+      count(w, km.B);
+    } else {
       ents[o] = msm_entry(km.kc ? (grp << km.kc) | (mag - 1) : grp * pl.B + (mag - 1), bidx | sign);
+      count(w, mag - 1);
+    }
   }
+}
+
+// One thread per scalar j of the row.  Every line of a batched MSM shares
+// the scalar row (ag-cuda-ec/src/multiexp.rs:21-81), so its digits -- and
+// hence the sorted order -- are the same for every line: the entries are
+// emitted and sorted ONCE, entry (w, j) at w * mpad + j with
+// key = (chunk(j) * W + w, |d| - 1) and value = j | sign, and the
+// accumulation walks the sorted list once per line (base and bucket offsets
+// per line).
+template <class C>
+__global__ void __launch_bounds__(MSM_THREADS)
+    msm_digits_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, size_t mpad, KeyMap km,
+                      uint64_t* __restrict__ ents) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= mpad) return;
+  msm_digits_one<C, false>(scalars, g, pl, mpad, km, ents, j, nullptr);
+}
+
+// The same entries for the c = 20 window blocks (msm_sort_fused), each
+// counted in its window's two 10-bit digit histograms as it is written:
+// MSM_HIST_SCALARS scalars per 1024-thread workgroup into LDS counters (W x
+// 8 KB), then one global atomic per non-zero counter into ghist -- the
+// histogram pass rocPRIM's onesweep would run over every block's 2^26 entries
+// again (0.14 ms per window at 2^26).  Counters are 16-bit, two per LDS word
+// (W x 4 KB: three workgroups per CU), so a workgroup counts at most 2^15
+// scalars (a counter never exceeds 2^15, whatever the digits).
+constexpr uint32_t MSM_HIST_THREADS = 1024;
+constexpr uint32_t MSM_HIST_SCALARS = 1u << 15;
+template <class C>
+__global__ void __launch_bounds__(MSM_HIST_THREADS)
+    msm_digits_hist_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, size_t mpad, KeyMap km,
+                           uint64_t* __restrict__ ents, uint32_t* __restrict__ ghist) {
+  extern __shared__ uint32_t lhist[];
+  const uint32_t nb = pl.W * 1024;  // words of two counters
+  for (uint32_t i = threadIdx.x; i < nb; i += MSM_HIST_THREADS) lhist[i] = 0;
+  __syncthreads();
+  const size_t j0 = (size_t)blockIdx.x * MSM_HIST_SCALARS;
+  const size_t j1 = j0 + MSM_HIST_SCALARS < mpad ? j0 + MSM_HIST_SCALARS : mpad;
+  for (size_t j = j0 + threadIdx.x; j < j1; j += MSM_HIST_THREADS)
+    msm_digits_one<C, true>(scalars, g, pl, mpad, km, ents, j, lhist);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nb; i += MSM_HIST_THREADS) {
+    const uint32_t h = lhist[i];
+    if (h & 0xffffu) atomicAdd(&ghist[2 * i], h & 0xffffu);
+    if (h >> 16) atomicAdd(&ghist[2 * i + 1], h >> 16);
+  }
+}
+
+// Exclusive scan of each 1024-bin histogram (one workgroup per (window,
+// place)): the global digit offsets of msm_sort_fused.
+template <int THREADS = 1024>  // a template: this header is included by one translation unit per curve
+__global__ void __launch_bounds__(THREADS) msm_hist_scan_kernel(uint32_t* __restrict__ ghist) {
+  using Scan = hipcub::BlockScan<uint32_t, THREADS>;
+  __shared__ typename Scan::TempStorage ts;
+  uint32_t* h = ghist + (size_t)blockIdx.x * THREADS;
+  uint32_t v = h[threadIdx.x];
+  Scan(ts).ExclusiveSum(v, v);
+  h[threadIdx.x] = v;
 }
 
 // ---------------------------------------------------------------------------
@@ -1217,6 +1344,11 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   const int cfg = pw ? msm_sort_cfg() : 0;
   const size_t sort_n = pw && !pw_one ? mpad : total;  // one sort per block, or one sort of all blocks
   const int sort_bits = pw ? (int)(pw_one ? pl.c + wbits : pl.c) : key_bits;
+  // the c = 20 window blocks (2^24 terms and up): digit histograms counted by
+  // the digits kernel, onesweep without its histogram pass (msm_sort_fused)
+  const bool fused = msm_fused_hist_enabled() && sort_mode == ECG_SORT_PW_BLOCK && pl.c == 20 && cfg == 2 &&
+                     sort_n >= ((size_t)1 << 22) && sort_n < 0xffffffffull && pl.W * 8192u <= 160u * 1024u;
+  void* hist = nullptr;
   if (do_acc || phase == CORE_RESERVE) {
   ECG_TRY(ws_get(ctx, "msm_e0", total * 8, &e0));
   ECG_TRY(ws_get(ctx, "msm_e1", total * 8, &e1));
@@ -1227,7 +1359,12 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   ECG_TRY(ws_get(ctx, "msm_recs2", 2 * nseg1 * sizeof(X), &rc2));
   ECG_TRY(ws_get(ctx, "msm_rkeys2", 2 * nseg1 * 4, &rk2));
   size_t tmp_bytes = 0;
-  ECG_HIP(msm_sort(cfg, nullptr, tmp_bytes, (uint64_t*)e0, (uint64_t*)e1, sort_n, 0, sort_bits, s));
+  if (fused) {
+    ECG_HIP(msm_sort_fused(nullptr, tmp_bytes, (uint64_t*)e0, (uint64_t*)e1, (unsigned int)sort_n, nullptr, s));
+    ECG_TRY(ws_get(ctx, "msm_hist", (size_t)pl.W * 2048 * 4, &hist));
+  } else {
+    ECG_HIP(msm_sort(cfg, nullptr, tmp_bytes, (uint64_t*)e0, (uint64_t*)e1, sort_n, 0, sort_bits, s));
+  }
   ECG_TRY(ws_get(ctx, "msm_sort_tmp", tmp_bytes, &tmp));
   if (msm_short_runs()) {  // the short pass runs at the first level below msm_short_max_recs records
     void* ks;
@@ -1259,9 +1396,23 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     }
   }
 
-  hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(mpad, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
-                     (const uint4*)d_scalars, g, pl, mpad, km, (uint64_t*)e0);
-  ECG_HIP(hipGetLastError());
+  if (fused) {
+    const uint32_t lds = pl.W * 4096u;
+    ECG_HIP(hipMemsetAsync(hist, 0, (size_t)pl.W * 2048 * 4, s));
+    // > 64 KB of dynamic LDS needs the attribute (a host-side call; set per launch, whatever device)
+    ECG_HIP(hipFuncSetAttribute((const void*)msm_digits_hist_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+    hipLaunchKernelGGL(msm_digits_hist_kernel<C>, dim3((uint32_t)((mpad + MSM_HIST_SCALARS - 1) / MSM_HIST_SCALARS)),
+                       dim3(MSM_HIST_THREADS), lds, s, (const uint4*)d_scalars, g, pl, mpad, km, (uint64_t*)e0,
+                       (uint32_t*)hist);
+    ECG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(msm_hist_scan_kernel<1024>, dim3(pl.W * 2), dim3(1024), 0, s, (uint32_t*)hist);
+    ECG_HIP(hipGetLastError());
+  } else {
+    hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(mpad, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                       (const uint4*)d_scalars, g, pl, mpad, km, (uint64_t*)e0);
+    ECG_HIP(hipGetLastError());
+  }
 
   // ---- group the (key, value) entries by bucket: rocPRIM onesweep radix sort
   // (an MSD counting sort with 10-bit coarse bins was measured 3x slower:
@@ -1274,8 +1425,13 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   // where it was and yields exactly the per-block result.  Per-block sorts
   // of <= 2^22 entries took rocPRIM's small-input path (10 launches per block
   // at 2^20: 2.7 of the 7.1 ms MSM) or onesweep launch tails.
-  for (size_t o = 0; o < total; o += sort_n)
-    ECG_HIP(msm_sort(cfg, tmp, tmp_bytes, (uint64_t*)e0 + o, (uint64_t*)e1 + o, sort_n, 0, sort_bits, s));
+  for (size_t o = 0, w = 0; o < total; o += sort_n, w++) {
+    if (fused)
+      ECG_HIP(msm_sort_fused(tmp, tmp_bytes, (uint64_t*)e0 + o, (uint64_t*)e1 + o, (unsigned int)sort_n,
+                             (unsigned int*)hist + w * 2048, s));
+    else
+      ECG_HIP(msm_sort(cfg, tmp, tmp_bytes, (uint64_t*)e0 + o, (uint64_t*)e1 + o, sort_n, 0, sort_bits, s));
+  }
 
   // one launch over every segment: per-block launches, each started as soon
   // as its block was sorted on a second stream, measured 6 ms slower at 2^26

@@ -547,3 +547,50 @@ def test_msm_per_block_sort_pinned_window(gpu_programs, cname, cid, n):
             assert same_point(cid, got[0], cpu), (w, bases is prep)
     prep.free()
     d_b.free()
+
+
+_FUSED_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import ecgpu
+cname, a, b, path = sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+E = np.load(path)
+prog = ecgpu.program(ecgpu.Device(0))
+n = E.shape[0]
+d_b = ecgpu.gen_bases_dev(prog, cname, a, b, n)
+d_e = ecgpu.DeviceBuffer.upload(prog, E)
+prep = ecgpu.prepare_bases(prog, cname, d_b, n)
+out = ecgpu.msm_dev(prog, cname, prep, d_e, n)
+print(" ".join("%x" % int(v) for v in out))
+"""
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_fused_histogram_sort_2p24(gpu_programs, cname, cid, tmp_path):
+    """The opt-in sort without onesweep's histogram pass (ECG_MSM_FUSED_HIST=1:
+    digit counts from msm_digits_hist_kernel, rocPRIM's onesweep iterations
+    on them) at the headline plan (c = 20, PW_BLOCK), in a child process (the
+    switch is read once per process), on skewed scalars: a third zero, a
+    third r - 1, the rest uniform -- bins far past 2^15 entries -- against the
+    known answer."""
+    import os
+    import subprocess
+    import sys
+
+    cv = po.CURVES[cname]
+    n = 1 << 24
+    a, b = 0x77AA5511, 0x2B3C
+    E = rand_scalars_np(cv, n, 9191 + cid)
+    E[0::3] = 0
+    E[1::3] = co.u64arr([cv.fr.modulus - 1], 4)[0]
+    path = str(tmp_path / "scal.npy")
+    np.save(path, E)
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "0g-ec-gpu_amd")
+    env = dict(os.environ, ECG_MSM_FUSED_HIST="1")
+    res = subprocess.run([sys.executable, "-c", _FUSED_CHILD, pkg, cname, str(a), str(b), path], env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-2000:]
+    got = np.array([int(x, 16) for x in res.stdout.split()], dtype=np.uint64)
+    kat = co.kat_scalar(cid, a, b, E, nthreads=16)
+    assert same_point(cid, got, co.gen_mul(cid, kat))
