@@ -538,3 +538,36 @@ def test_config4_msm_2p26_grid_split(gpu_programs, cname, cid):
             p.close()
         prep.free()
         d_sc.free()
+
+
+def test_msm_dist_grid_failure_semantics(gpu_programs):
+    """The grid split shares the range split's status exchange: a rank with an
+    unknown curve or an abort makes every rank return the same error, and the
+    ranks stay usable (3 ranks, one GPU, host transport)."""
+    world = 3
+    progs = _host_ranks(gpu_programs[1][0], world)
+    try:
+        cid, cname = 0, "bls12_381"
+        n = 777
+        B = co.gen_bases(cid, 5, 7, n, 8)
+        E = rand_fr(po.BLS12_381_FR, n, 12)
+        d_b = [ecgpu.DeviceBuffer.upload(p, B) for p in progs]
+        d_e = [ecgpu.DeviceBuffer.upload(p, E) for p in progs]
+
+        def grid(curves, aborts=(False,) * world):
+            return _run_ranks(world, lambda r: edist.msm_dist_grid(
+                progs[r], curves[r], d_b[r], d_e[r], n, maybe_abort=(lambda: True) if aborts[r] else None))
+
+        res = grid([cname, 9, cname])
+        assert not any(ok for ok, _ in res)
+        assert "rank 1 of 3 failed" in str(res[0][1]) and "rank 1 of 3 failed" in str(res[2][1])
+        res = grid([cname] * 3, aborts=(False, True, False))
+        assert all(isinstance(e, ecgpu.Aborted) for _, e in res), res
+        res = grid([cname] * 3)
+        want = co.jac_to_affine(cid, co.multiexp_cpu(cid, B, E, nthreads=8))
+        assert all(ok and (co.jac_to_affine(cid, v) == want).all() for ok, v in res), res
+        for b in d_b + d_e:
+            b.free()
+    finally:
+        for p in progs:
+            p.close()
