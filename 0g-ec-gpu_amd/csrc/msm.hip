@@ -234,7 +234,27 @@ int msm_grid_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_
   const unsigned __int128 T = (unsigned __int128)W * n;
   const uint64_t a = (uint64_t)(T * (unsigned)rank / (unsigned)nranks);
   const uint64_t b = (uint64_t)(T * (unsigned)(rank + 1) / (unsigned)nranks);
+  // one core call over the rank's window blocks (msm_grid_t); ECG_MSM_GRID_PIECES=1 runs the
+  // former piece-by-piece form (A/B)
+  static const bool by_pieces = [] {
+    const char* e = getenv("ECG_MSM_GRID_PIECES");
+    return e && e[0] == '1';
+  }();
+  // (a share of more than 16 windows -- small n, few ranks -- runs piece by piece)
+  const bool one_call = !by_pieces && (a >= b || (b - 1) / n - a / n + 1 <= 16);
   auto run = [&](BaseForm f) -> int {
+    if (one_call) {
+      if (a >= b) {  // no grid cell for this rank (more ranks than cells): the identity
+        if (pieces) *pieces = 0;
+        return o->point_sum(nullptr, 0, out_jac);
+      }
+      const uint32_t w0 = (uint32_t)(a / n), wl = (uint32_t)((b - 1) / n);
+      if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144, per device pass
+      ECG_TRY(o->grid(ctx, d_bases, d_scalars, n, w0, wl - w0 + 1, (size_t)(a - (uint64_t)w0 * n),
+                      (size_t)(b - (uint64_t)wl * n), out_jac, s, f));
+      if (pieces) *pieces = 1;
+      return ECG_OK;
+    }
     const size_t stride = f.prepared ? msm_prepared_stride(curve_id, 0) : 2 * lq * 8;
     std::vector<uint64_t> parts;
     int np = 0;

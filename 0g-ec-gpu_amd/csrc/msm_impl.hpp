@@ -225,12 +225,27 @@ struct MsmPlan {
 // chunks of clen = line_len / n_chunks terms (a remainder is ignored, as in
 // multiexp.cl:230), and task (line, chunk) computes
 //   sum_{i < clen} s[chunk*clen + i] * P[line*line_len + chunk*clen + i].
+// Window blocks of one rank's share of the grid split (msm_grid_t): block i
+// holds window w0 + i over terms [lo[i], lo[i] + len[i]) of the n-term row,
+// padded to mp[i] entries (a multiple of the accumulation segment) at
+// offset off[i] of the entry list.
+constexpr uint32_t MSM_GRID_MAXB = 16;
+struct GridBlocks {
+  uint32_t nb;
+  uint64_t total;
+  uint64_t off[MSM_GRID_MAXB];
+  uint64_t len[MSM_GRID_MAXB];
+  uint64_t lo[MSM_GRID_MAXB];
+  uint64_t mp[MSM_GRID_MAXB];
+};
+
 struct MsmGeom {
   uint32_t n_lines;
   uint32_t n_chunks;
   size_t line_len;
   size_t clen;
   uint32_t scalar_mont;  // scalars arrive as Montgomery Fr elements (to_bigint on device)
+  const GridBlocks* grid = nullptr;  // host-side: the grid split's window blocks (one task, one line)
   uint32_t tasks() const { return n_lines * n_chunks; }
 };
 
@@ -485,6 +500,33 @@ __global__ void __launch_bounds__(MSM_THREADS)
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= mpad) return;
   msm_digits_one<C, false>(scalars, g, pl, mpad, km, ents, j, nullptr);
+}
+
+// The grid split's entries (msm_grid_t): entry t of block i is term
+// lo[i] + t - off[i] in window w0 + i (its digit carries the chain of the
+// windows below it), or the block sentinel past len[i].
+template <class C>
+__global__ void __launch_bounds__(MSM_THREADS)
+    msm_digits_grid_kernel(const uint4* __restrict__ scalars, MsmGeom g, MsmPlan pl, KeyMap km, GridBlocks gb,
+                           uint64_t* __restrict__ ents) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= gb.total) return;
+  uint32_t i = 0;
+  while (i + 1 < gb.nb && t >= gb.off[i + 1]) i++;
+  const size_t j = t - gb.off[i];
+  if (j >= gb.len[i]) {
+    ents[t] = msm_entry((i << km.kc) | km.B, 0);
+    return;
+  }
+  const size_t term = gb.lo[i] + j;
+  uint32_t s[9];
+  load_scalar<C>(scalars, term, g.scalar_mont, s);
+  uint32_t carry = 0;
+  int32_t d = 0;
+  for (uint32_t wa = 0; wa <= pl.w0 + i; wa++) d = window_digit(s, wa, pl, carry);
+  const uint32_t mag = d < 0 ? (uint32_t)(-d) : (uint32_t)d;
+  const uint32_t sign = d < 0 ? 0x80000000u : 0u;
+  ents[t] = d == 0 ? msm_entry((i << km.kc) | km.B, 0) : msm_entry((i << km.kc) | (mag - 1), (uint32_t)term | sign);
 }
 
 // The same entries for the c = 20 window blocks (msm_sort_fused), each
@@ -1311,10 +1353,16 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   const uint32_t line_groups = pl.G / g.n_lines;  // n_chunks * W
   // window-padded keys (KeyMap) when every (window, line) block is one group
   // and large enough for a sort of its own
-  const int sort_mode = msm_sort_mode(pl, m, g.n_chunks, line_groups);
+  // the grid split's blocks always carry window-padded keys, sorted block by block
+  const int sort_mode = g.grid ? ECG_SORT_PW_BLOCK : msm_sort_mode(pl, m, g.n_chunks, line_groups);
   const bool pw = sort_mode != ECG_SORT_GLOBAL;
-  const size_t mpad = pw ? (m + pl.seg - 1) / pl.seg * pl.seg : m;
-  const size_t total = (size_t)pl.W * mpad;
+  const GridBlocks* const gb = g.grid;  // grid split: blocks of their own lengths (window-padded keys)
+  size_t mpad = pw ? (m + pl.seg - 1) / pl.seg * pl.seg : m;
+  if (gb) {
+    mpad = 0;
+    for (uint32_t i = 0; i < gb->nb; i++) mpad = std::max<size_t>(mpad, gb->mp[i]);
+  }
+  const size_t total = gb ? gb->total : (size_t)pl.W * mpad;
   const KeyMap km{pw ? pl.c : 0u, pl.B, line_groups * pl.B};
   int key_bits = 1;
   while ((1ull << key_bits) <= km.sentinel) key_bits++;
@@ -1346,7 +1394,7 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   const int sort_bits = pw ? (int)(pw_one ? pl.c + wbits : pl.c) : key_bits;
   // the c = 20 window blocks (2^24 terms and up): digit histograms counted by
   // the digits kernel, onesweep without its histogram pass (msm_sort_fused)
-  const bool fused = msm_fused_hist_enabled() && sort_mode == ECG_SORT_PW_BLOCK && pl.c == 20 && cfg == 2 &&
+  const bool fused = !gb && msm_fused_hist_enabled() && sort_mode == ECG_SORT_PW_BLOCK && pl.c == 20 && cfg == 2 &&
                      sort_n >= ((size_t)1 << 22) && sort_n < 0xffffffffull && pl.W * 8192u <= 160u * 1024u;
   void* hist = nullptr;
   if (do_acc || phase == CORE_RESERVE) {
@@ -1408,6 +1456,10 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     ECG_HIP(hipGetLastError());
     hipLaunchKernelGGL(msm_hist_scan_kernel<1024>, dim3(pl.W * 2), dim3(1024), 0, s, (uint32_t*)hist);
     ECG_HIP(hipGetLastError());
+  } else if (gb) {
+    hipLaunchKernelGGL(msm_digits_grid_kernel<C>, dim3(blocks_for(total, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                       (const uint4*)d_scalars, g, pl, km, *gb, (uint64_t*)e0);
+    ECG_HIP(hipGetLastError());
   } else {
     hipLaunchKernelGGL(msm_digits_kernel<C>, dim3(blocks_for(mpad, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
                        (const uint4*)d_scalars, g, pl, mpad, km, (uint64_t*)e0);
@@ -1425,7 +1477,12 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   // where it was and yields exactly the per-block result.  Per-block sorts
   // of <= 2^22 entries took rocPRIM's small-input path (10 launches per block
   // at 2^20: 2.7 of the 7.1 ms MSM) or onesweep launch tails.
-  for (size_t o = 0, w = 0; o < total; o += sort_n, w++) {
+  if (gb) {  // one sort per block, each over its own padded length
+    for (uint32_t i = 0; i < gb->nb; i++)
+      ECG_HIP(msm_sort(cfg, tmp, tmp_bytes, (uint64_t*)e0 + gb->off[i], (uint64_t*)e1 + gb->off[i], gb->mp[i], 0,
+                       sort_bits, s));
+  }
+  for (size_t o = 0, w = 0; !gb && o < total; o += sort_n, w++) {
     if (fused)
       ECG_HIP(msm_sort_fused(tmp, tmp_bytes, (uint64_t*)e0 + o, (uint64_t*)e1 + o, (unsigned int)sort_n,
                              (unsigned int*)hist + w * 2048, s));
@@ -1878,6 +1935,60 @@ int msm_piece_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t
     ECG_HIP(hipStreamSynchronize(s));
     msm_host_fold_bits<C>(win, e, total);
   }
+  host::hto_jac_norm(total, out_jac);
+  return ECG_OK;
+}
+
+// One rank's share of the grid split in ONE core call: windows [w0, w0 + nw)
+// of the n-term plan -- window w0 over terms [lo_first, n) (or [lo_first,
+// hi_last) when nw = 1), the middle windows over all n terms, window
+// w0 + nw - 1 over [0, hi_last) -- as window blocks of their own lengths: one
+// digits launch, one sort per block, one accumulation, one reduction and one
+// host fold.  (msm_piece_t's core call per piece paid a partly filled
+// accumulation round, a reduction and a scalar read per piece: DESIGN.md §7.)
+template <class C>
+int msm_grid_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t n, uint32_t w0, uint32_t nw,
+               size_t lo_first, size_t hi_last, uint64_t* out_jac, hipStream_t s, BaseForm bf) {
+  using HX = host::HPoint<HostF<C>>;
+  using X = XYZZ<typename C::Fq>;
+  if (bf.tab_c) {
+    set_error("multiexp: the grid split needs plain prepared bases or [x, y] bases, not a window table");
+    return ECG_ERR_INVALID;
+  }
+  MsmPlan pl = make_plan(n, (uint32_t)C::FrParams::BITS);
+  if (nw == 0 || nw > MSM_GRID_MAXB || w0 + nw > pl.W || n > 0x7fffffffull || lo_first >= n || hi_last > n ||
+      hi_last == 0 || (nw == 1 && hi_last <= lo_first)) {
+    set_error("multiexp: grid share [window %u term %zu, window %u term %zu) outside the %u x %zu grid", w0,
+              lo_first, w0 + nw - 1, hi_last, pl.W, n);
+    return ECG_ERR_INVALID;
+  }
+  GridBlocks gb{};
+  gb.nb = nw;
+  uint64_t off = 0;
+  for (uint32_t i = 0; i < nw; i++) {
+    const uint64_t lo = i == 0 ? lo_first : 0, hi = i + 1 == nw ? hi_last : n;
+    gb.off[i] = off;
+    gb.lo[i] = lo;
+    gb.len[i] = hi - lo;
+    gb.mp[i] = (gb.len[i] + pl.seg - 1) / pl.seg * pl.seg;
+    off += gb.mp[i];
+  }
+  gb.total = off;
+  pl.wd = pl.W;
+  pl.w0 = w0;
+  pl.W = nw;
+  pl.G = nw;
+  plan_reduction(pl);  // the caller resets the msm_accumulate timer
+  MsmGeom g{1, 1, n, n, 0};
+  g.grid = &gb;
+  void* d_sums;
+  ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums, bf.prepared));
+  const MsmPlan e = msm_eff_plan<C>(pl);
+  X* win;  // mapped pinned host memory (msm_sums_to_std_kernel)
+  ECG_TRY(hws_get(ctx, "msm_sums_host", msm_single_sums(e) * sizeof(X), (void**)&win));
+  ECG_HIP(hipStreamSynchronize(s));
+  HX total = HX::zero();
+  msm_host_fold_bits<C>(win, e, total);
   host::hto_jac_norm(total, out_jac);
   return ECG_OK;
 }

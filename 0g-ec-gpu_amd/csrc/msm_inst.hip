@@ -37,6 +37,7 @@ MsmOps ECG_OPS_NAME = {&msm_single_t<InstCurve>,        &batch_entry,
                        &point_sum_host_t<InstCurve>,    &gen_bases_t<InstCurve>,
                        &msm_pass_terms<InstCurve>,      &msm_host_t<InstCurve>,
                        &msm_base_record_bytes<InstCurve>, &msm_plan_info_t<InstCurve>,
-                       &msm_piece_t<InstCurve>};
+                       &msm_piece_t<InstCurve>,
+                       &msm_grid_t<InstCurve>};
 
 }  // namespace ecg

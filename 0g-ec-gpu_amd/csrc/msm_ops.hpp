@@ -28,6 +28,9 @@ struct MsmOps {
   // windows [w0, w0 + nwin) of the n_plan-term plan over m terms (msm_piece_t)
   int (*piece)(ecg_ctx*, const void* d_bases, const void* d_scalars, size_t m, size_t n_plan, uint32_t w0,
                uint32_t nwin, uint64_t* out_jac, hipStream_t, BaseForm bf);
+  // a rank's whole grid share in one core call (msm_grid_t)
+  int (*grid)(ecg_ctx*, const void* d_bases, const void* d_scalars, size_t n, uint32_t w0, uint32_t nw,
+              size_t lo_first, size_t hi_last, uint64_t* out_jac, hipStream_t, BaseForm bf);
 };
 
 // This rank's share of an n-term MSM split over a grid of (window x term)

@@ -129,10 +129,12 @@ def parse(argv=None):
                          "ranks on one GPU, which RCCL refuses)")
     ap.add_argument("--single-device", action="store_true",
                     help="every rank on GPU 0 (with --transport host: N-rank rehearsal on a one-GPU box)")
-    ap.add_argument("--msm-split", choices=("range", "grid"), default="range",
+    ap.add_argument("--msm-split", choices=("auto", "range", "grid"), default="auto",
                     help="N > 1 MSM split: 'range' = contiguous term shards (multiexp.rs:332-336, "
                          "ecg_msm_dist); 'grid' = every rank holds all bases and scalars and runs 1/N of the "
-                         "(window x term) grid of the whole-n plan (ecg_msm_dist_grid, SURVEY §8(e))")
+                         "(window x term) grid of the whole-n plan (ecg_msm_dist_grid, SURVEY §8(e)); 'auto' = "
+                         "grid for BLS12-381 at N >= 4, where it measured faster per rank, else range "
+                         "(DESIGN.md §7)")
     ap.add_argument("--unprepared", action="store_true",
                     help="time the MSM over [x, y] bases (conversion to the kernel layout inside every step)")
     return ap.parse_args(argv)
@@ -244,7 +246,10 @@ def main():
 
     # ------------------------------------------------------------ MSM inputs (HBM-resident)
     n_total = 1 << args.msm_log
-    grid = world > 1 and args.msm_split == "grid"
+    split = args.msm_split
+    if split == "auto":  # per-rank times on one GPU, profiles/r05/grid_split_probe_onecall_*.log
+        split = "grid" if world >= 4 and cid == 0 else "range"
+    grid = world > 1 and split == "grid"
     all_shards = None
     if grid:  # replicated operands: every rank holds all n_total bases and the scalars of every shard
         all_shards = [msm_shard(r, world, n_total, r_int) for r in range(world)]
@@ -773,7 +778,7 @@ def main():
                    "(ecg_msm_prepare_bases, upload_multiexp_bases's role)"),
         "config": {"workload": f"{args.curve} G1 MSM 2^{args.msm_log} terms sharded over {world} GPU(s) "
                                f"+ Fr NTT 2^{log_n} per GPU", "msm_terms": n_total, "ntt_log_n": log_n,
-                   "msm_split": args.msm_split if world > 1 else None,
+                   "msm_split": split if world > 1 else None,
                    "parallelism": ((f"grid split (window x term) x{world}, replicated bases + " if grid
                                     else f"range-shard x{world} + ")
                                    + ("RCCL" if args.transport == "rccl" else "host-group (rehearsal)")

@@ -297,6 +297,28 @@ def test_bench_main_world2_grid_split():
 
 
 @pytest.mark.timeout(300)
+def test_bench_main_world4_auto_split():
+    """bench.main() at N = 4 with the default --msm-split auto: BLS12-381 takes
+    the grid split from N = 4 on; the KAT and the NTT digests
+    hold and the line records the split."""
+    import multiprocessing as mp
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_main_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(280)
+    outs = dict(q.get(timeout=10) for _ in range(4))
+    assert all(p.exitcode == 0 for p in procs)
+    line = json.loads(outs[0].strip().splitlines()[-1])
+    assert line["n_gpus"] == 4 and line["config"]["msm_split"] == "grid"
+    assert line["checks"]["msm_kat_2^10"] is True and line["checks"]["ntt_dist_4gpu_vs_parallel_fft_2^8"] is True
+
+
+@pytest.mark.timeout(300)
 def test_bench_main_world2_failing_rank():
     """bench.main() at N = 2 with rank 1's distributed MSM failing locally
     (an emulated allocation failure inside ecg_msm_dist): the status rides in
