@@ -267,12 +267,15 @@ int comm_agree(ecg_ctx* ctx, int local_rc, const uint64_t* agree, int n_agree, c
 // result -- or the same error (the lowest failing rank's).  `rc` and the
 // partial in rec come from this rank's local step; nothing here allocates
 // (comm_exchange_rec), so a failed local step still joins the exchange.
+// `shape` (the grid split's n; 0 for the range split, whose shards may differ)
+// rides in the record's curve word, so ranks called with different whole-MSM
+// sizes -- whose grid shares would overlap or leave gaps -- all fail.
 static int dist_fold_partials(ecg_ctx* ctx, int rc, int curve_id, uint64_t* rec, size_t rec_words, uint64_t* out_jac,
-                              hipStream_t s, const char* what) {
+                              hipStream_t s, const char* what, uint64_t shape = 0) {
   const std::string local_msg = rc != ECG_OK ? last_error_text() : "";
   if (rc != ECG_OK) (void)hipStreamSynchronize(s);  // the failed run's work is done or abandoned
   rec[0] = (uint64_t)(int64_t)rc;
-  rec[1] = (uint64_t)(uint32_t)curve_id;
+  rec[1] = (uint64_t)(uint8_t)curve_id | shape << 8;
   const int P = ctx->comm_size;
   // one exchange, no allocation on this path: every rank joins it whatever
   // its local step did (comm_exchange_rec)
@@ -293,9 +296,10 @@ static int dist_fold_partials(ecg_ctx* ctx, int rc, int curve_id, uint64_t* rec,
   const size_t pw = 3 * (size_t)fq_limbs64(curve_id);
   std::vector<uint64_t> parts(pw * P);
   for (int r = 0; r < P; r++) {
-    if ((int)all[(size_t)r * rec_words + 1] != curve_id) {
-      set_error("%s: rank %d ran curve %d, this rank curve %d", what, r, (int)all[(size_t)r * rec_words + 1],
-                curve_id);
+    const uint64_t w = all[(size_t)r * rec_words + 1];
+    if (w != rec[1]) {
+      set_error("%s: rank %d ran curve %d over n = %llu, this rank curve %d over n = %llu", what, r, (int)(w & 0xff),
+                (unsigned long long)(w >> 8), curve_id, (unsigned long long)shape);
       return ECG_ERR_INVALID;
     }
     memcpy(&parts[pw * r], &all[(size_t)r * rec_words + 2], pw * 8);
@@ -499,7 +503,7 @@ int ecg_msm_dist_grid_ex(ecg_ctx* ctx, int curve_id, const void* d_bases, const 
     memcpy(out_jac, rec + 2, 3 * (size_t)fq_limbs64(curve_id) * 8);
     return kt_collect(ctx);
   }
-  return dist_fold_partials(ctx, rc, curve_id, rec, 2 + PW, out_jac, s, "ecg_msm_dist_grid");
+  return dist_fold_partials(ctx, rc, curve_id, rec, 2 + PW, out_jac, s, "ecg_msm_dist_grid", (uint64_t)n);
 }
 
 int ecg_msm_dist_grid(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scalars, size_t n,

@@ -60,8 +60,9 @@ int ws_get(ecg_ctx* ctx, const char* name, size_t bytes, void** out) {
   }
   if (b.bytes < bytes) {
     if (b.ptr) {
-      // the buffer may still be in use by queued work
-      ECG_HIP(hipStreamSynchronize(ctx->stream));
+      // the buffer may still be in use by queued work on any stream the caller
+      // chose (pick_stream), not only ctx->stream: drain the device (growth is rare)
+      ECG_HIP(hipDeviceSynchronize());
       ECG_HIP(hipFree(b.ptr));
       b.ptr = nullptr;
       b.bytes = 0;
@@ -84,7 +85,9 @@ int hws_get(ecg_ctx* ctx, const char* name, size_t bytes, void** out, void** dev
   if (bytes == 0) bytes = 16;
   if (b.bytes < bytes) {
     if (b.ptr) {
-      ECG_HIP(hipStreamSynchronize(ctx->stream));  // a queued copy may still target it
+      // a queued copy or kernel (on ctx->stream, the caller's stream or the
+      // pipeline's copy stream) may still target it: drain the device
+      ECG_HIP(hipDeviceSynchronize());
       ECG_HIP(hipHostFree(b.ptr));
       b.ptr = nullptr;
       b.bytes = 0;

@@ -136,6 +136,20 @@ static int prepared_lookup(ecg_ctx* ctx, int curve_id, const void* d_bases, size
     prepared_drop(start, e.nonce);
     return ECG_OK;
   }
+  // a refusal of a deferred entry waits for its header check first: a stale
+  // entry (the address now holds someone else's [x, y] bases) is dropped and
+  // the call goes on unprepared, instead of refusing every later call
+  auto refuse = [&]() -> int {
+    if (defer && defer->pending) {
+      (void)hipStreamSynchronize(s);
+      if (!prepared_confirm(*defer)) {
+        *defer = PrepCheck{};
+        (void)hipGetLastError();
+        return ECG_OK;
+      }
+    }
+    return ECG_ERR_INVALID;
+  };
   if (e.device != ctx->device) {
     set_error("%s: the prepared bases live on device %d, the context is on device %d", what, e.device, ctx->device);
     return ECG_ERR_INVALID;
@@ -144,13 +158,13 @@ static int prepared_lookup(ecg_ctx* ctx, int curve_id, const void* d_bases, size
   if (off % e.stride) {
     set_error("%s: pointer %zu bytes into prepared bases is not on a base boundary (%zu bytes per base)", what, off,
               e.stride);
-    return ECG_ERR_INVALID;
+    return refuse();
   }
   const size_t avail = e.n - off / e.stride;
   if (e.curve != curve_id || n > avail) {
     set_error("%s: prepared bases hold %zu bases of curve %d from this pointer, the call reads %zu of curve %d", what,
               avail, e.curve, n, curve_id);
-    return ECG_ERR_INVALID;
+    return refuse();
   }
   bf->prepared = true;
   bf->tab_c = e.tab_c;
@@ -201,7 +215,9 @@ int msm_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_scala
   ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n, "multiexp", &bf, s, &chk));
   int rc = o->single(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0, bf);
   (void)hipStreamSynchronize(s);
-  if (rc == ECG_OK && !prepared_confirm(chk))  // released behind the library's back: not our records
+  // released behind the library's back: not our records (on every return path,
+  // so a failed first run still drops the stale entry)
+  if (!prepared_confirm(chk))
     rc = o->single(ctx, d_bases, d_scalars, n, out_jac, s, abort_cb, user, scalar_mont != 0, BaseForm{});
   return rc;
 }
@@ -226,8 +242,13 @@ int msm_grid_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_
   PrepCheck chk;
   ECG_TRY(prepared_lookup(ctx, curve_id, d_bases, n, "multiexp", &bf, s, &chk));
   if (bf.tab_c) {
-    set_error("msm_dist_grid: the bases are a window table; the grid split needs plain prepared or [x, y] bases");
-    return ECG_ERR_INVALID;
+    (void)hipStreamSynchronize(s);
+    if (prepared_confirm(chk)) {
+      set_error("msm_dist_grid: the bases are a window table; the grid split needs plain prepared or [x, y] bases");
+      return ECG_ERR_INVALID;
+    }
+    bf = BaseForm{};  // a stale table entry: the pointer holds [x, y] bases
+    chk = PrepCheck{};
   }
   const size_t lq = fq_limbs64(curve_id);
   // grid entries e = w n + t (window-major); this rank's range [a, b)
@@ -285,7 +306,7 @@ int msm_grid_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_
   };
   int rc = run(bf);
   (void)hipStreamSynchronize(s);
-  if (rc == ECG_OK && !prepared_confirm(chk)) rc = run(BaseForm{});  // stale: the pointer holds [x, y] bases
+  if (!prepared_confirm(chk)) rc = run(BaseForm{});  // stale: the pointer holds [x, y] bases
   return rc;
 }
 
@@ -393,7 +414,7 @@ int msm_batch_run(ecg_ctx* ctx, int curve_id, const void* d_bases, size_t n_base
   int rc = o->batch(ctx, d_bases, d_scalars, (uint32_t)n_lines, (uint32_t)n_chunks, line_len, scalar_mont != 0,
                     window_bits, out_jac, s, bf);
   (void)hipStreamSynchronize(s);
-  if (rc == ECG_OK && !prepared_confirm(chk))  // released behind the library's back: not our records
+  if (!prepared_confirm(chk))  // released behind the library's back: not our records
     rc = o->batch(ctx, d_bases, d_scalars, (uint32_t)n_lines, (uint32_t)n_chunks, line_len, scalar_mont != 0,
                   window_bits, out_jac, s, BaseForm{});
   return rc;

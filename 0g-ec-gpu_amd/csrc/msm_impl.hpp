@@ -1899,6 +1899,26 @@ void msm_host_fold_bits(const XYZZ<typename C::Fq>* sums, const MsmPlan& e, host
   total = host::hadd_pts(total, host::hxyzz_from_jac(acc));
 }
 
+// The window sums of a single-task core call, on the host after s is drained.
+// The reduced-radix pipeline wrote them into the mapped pinned buffer
+// "msm_sums_host" already (msm_sums_to_std_kernel); the boundary-form pipeline
+// (ECG_MSM_RR=0) leaves them in device memory at d_sums, so they are copied.
+template <class X>
+int msm_sums_to_host(ecg_ctx* ctx, const void* d_sums, size_t count, hipStream_t s, X** win) {
+  const size_t bytes = count * sizeof(X);
+  bool mapped = false;
+  auto it = ctx->hws.find("msm_sums_host");
+  if (it != ctx->hws.end() && it->second.ptr && it->second.bytes >= bytes) {
+    void* dev = nullptr;
+    ECG_HIP(hipHostGetDevicePointer(&dev, it->second.ptr, 0));
+    mapped = dev == d_sums;
+  }
+  ECG_TRY(hws_get(ctx, "msm_sums_host", bytes, (void**)win));  // no growth when mapped
+  if (!mapped) ECG_HIP(hipMemcpyAsync(*win, d_sums, bytes, hipMemcpyDeviceToHost, s));
+  ECG_HIP(hipStreamSynchronize(s));
+  return ECG_OK;
+}
+
 // One piece of the (window x term) grid of an n_plan-term MSM: windows
 // [w0, w0 + nwin) of the n_plan-term plan over the m terms at d_bases /
 // d_scalars (views at the piece's first term).  Returns the piece's partial,
@@ -1930,9 +1950,8 @@ int msm_piece_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t
     void* d_sums;
     ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums, bf.prepared));
     const MsmPlan e = msm_eff_plan<C>(pl);
-    X* win;  // mapped pinned host memory (msm_sums_to_std_kernel)
-    ECG_TRY(hws_get(ctx, "msm_sums_host", msm_single_sums(e) * sizeof(X), (void**)&win));
-    ECG_HIP(hipStreamSynchronize(s));
+    X* win;
+    ECG_TRY(msm_sums_to_host(ctx, d_sums, msm_single_sums(e), s, &win));
     msm_host_fold_bits<C>(win, e, total);
   }
   host::hto_jac_norm(total, out_jac);
@@ -1984,9 +2003,8 @@ int msm_grid_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_t 
   void* d_sums;
   ECG_TRY(msm_core_t<C>(ctx, d_bases, d_scalars, g, pl, s, &d_sums, bf.prepared));
   const MsmPlan e = msm_eff_plan<C>(pl);
-  X* win;  // mapped pinned host memory (msm_sums_to_std_kernel)
-  ECG_TRY(hws_get(ctx, "msm_sums_host", msm_single_sums(e) * sizeof(X), (void**)&win));
-  ECG_HIP(hipStreamSynchronize(s));
+  X* win;
+  ECG_TRY(msm_sums_to_host(ctx, d_sums, msm_single_sums(e), s, &win));
   HX total = HX::zero();
   msm_host_fold_bits<C>(win, e, total);
   host::hto_jac_norm(total, out_jac);
@@ -2058,10 +2076,8 @@ int msm_single_t(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, size_
     // window A / offset-bit sums -> host; Horner fold over windows (multiexp.rs:221-233)
     const MsmPlan e = msm_eff_plan<C>(pl);
     const size_t nw = msm_single_sums(e);
-    // the sums are in mapped host memory already (msm_sums_to_std_kernel)
     X* win;
-    ECG_TRY(hws_get(ctx, "msm_sums_host", nw * sizeof(X), (void**)&win));
-    ECG_HIP(hipStreamSynchronize(s));
+    ECG_TRY(msm_sums_to_host(ctx, d_sums, nw, s, &win));
     msm_host_fold_bits<C>(win, e, total_acc);
   }
   host::hto_jac_norm(total_acc, out_jac);

@@ -28,7 +28,9 @@ the distributed NTT (SHA-256 digests) against the same parallel_fft.  Rank 0
 at N=1 also times the CPU restatements as the baseline.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under
-torch.distributed.run (one process per GPU).
+torch.distributed.run (one process per GPU), or plain `python bench.py --gpus N`,
+which starts the N rank processes itself (launch_ranks) with the same
+environment the launcher gives them.
 """
 from __future__ import annotations
 
@@ -213,8 +215,69 @@ def block_digests(a: np.ndarray, world: int) -> list:
     return [hashlib.sha256(np.ascontiguousarray(a[r * m:(r + 1) * m]).tobytes()).hexdigest() for r in range(world)]
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv=None, grace_s: float = 60.0) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: start the N rank
+    processes here, one per GPU, with the environment torch.distributed.run
+    gives them (RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT), as the reference's MultiexpKernel spreads one
+    multiexp over every device it holds (multiexp.rs:324-367, fft.rs:216-243).
+    This parent never loads libecgpu or touches a GPU and never execs: the
+    children inherit stdout / stderr (rank 0 alone prints the JSON line), and
+    the exit code is the first failing rank's, after the others have been given
+    `grace_s` to stop on their own (a failed rank fails every rank through the
+    status records, comm.cpp) and are then killed."""
+    import signal
+    import subprocess
+
+    argv = sys.argv[1:] if argv is None else list(argv)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(sys.argv[0]), *argv], env=env,
+                                      start_new_session=True))
+    rc, first_fail = 0, None
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            if all(c is not None for c in codes):
+                break
+            failed = [c for c in codes if c not in (None, 0)]
+            if failed and first_fail is None:
+                first_fail = time.monotonic()
+                rc = failed[0]
+            if first_fail is not None and time.monotonic() - first_fail > grace_s:
+                for p in procs:
+                    if p.poll() is None:
+                        os.killpg(p.pid, signal.SIGKILL)
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+        raise
+    for r, p in enumerate(procs):
+        if p.returncode != 0:
+            print(f"bench: rank {r} of {n} exited with {p.returncode}", file=sys.stderr)
+            rc = rc or p.returncode
+    return 1 if rc and rc < 0 else rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -343,6 +343,42 @@ def test_bench_main_world2_failing_rank():
     assert '"metric"' not in outs[0]
 
 
+def _run_self_launch(world, extra_env=None, timeout=280):
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env.update({"OMP_NUM_THREADS": "2", **(extra_env or {})})
+    cmd = [sys.executable, os.path.join(ROOT, "tests", "bench_fake_ranks.py"), "--gpus", str(world),
+           "--steps", "2", "--warmup", "1", "--msm-log", "10", "--ntt-log", "8"]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.timeout(300)
+def test_bench_self_launch_world2():
+    """`bench.py --gpus 2` without torch.distributed.run: the process starts its
+    two rank processes itself (bench.launch_ranks), and exactly one JSON line
+    -- rank 0's -- comes out, recording both ranks' communicators."""
+    p = _run_self_launch(2)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["rccl"]["count"] == [2]
+    assert line["rccl"]["ranks"] == [0, 1] and line["rccl"]["distinct"] is True
+    assert line["checks"]["msm_kat_2^10"] is True and line["checks"]["ntt_dist_2gpu_vs_parallel_fft_2^8"] is True
+
+
+@pytest.mark.timeout(300)
+def test_bench_self_launch_failing_rank():
+    """A rank that fails makes the launching process exit non-zero, with no
+    JSON line and no rank left running."""
+    p = _run_self_launch(2, {"FAKE_FAIL_RANK": "1"})
+    assert p.returncode != 0
+    assert '"metric"' not in p.stdout
+    assert "rank 1 of 2 failed" in p.stderr
+
+
 def test_kat_scalar_regeneration_matches_single_rank():
     """bench.msm_kat_scalar over 3 regenerated shards == the KAT of the
     concatenated scalars: the N>1 check covers exactly the full workload."""

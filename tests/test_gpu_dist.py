@@ -563,6 +563,11 @@ def test_msm_dist_grid_failure_semantics(gpu_programs):
         assert "rank 1 of 3 failed" in str(res[0][1]) and "rank 1 of 3 failed" in str(res[2][1])
         res = grid([cname] * 3, aborts=(False, True, False))
         assert all(isinstance(e, ecgpu.Aborted) for _, e in res), res
+        # rank 2 is called with another whole-MSM size: its grid share would not tile
+        # the others', so every rank refuses the result (n rides in the record)
+        res = _run_ranks(world, lambda r: edist.msm_dist_grid(progs[r], cname, d_b[r], d_e[r], n - 100 if r == 2 else n))
+        assert not any(ok for ok, _ in res), res
+        assert all("n = " in str(e) for _, e in res), res
         res = grid([cname] * 3)
         want = co.jac_to_affine(cid, co.multiexp_cpu(cid, B, E, nthreads=8))
         assert all(ok and (co.jac_to_affine(cid, v) == want).all() for ok, v in res), res

@@ -7,6 +7,8 @@ checked against the CPU oracle's multiexp_cpu restatement, the committed
 golden fixtures, and at large sizes the known-answer construction
 P_i = (a + i b) G  =>  sum s_i P_i = (sum s_i (a + i b) mod r) G."""
 import ctypes
+import os
+import sys
 
 import numpy as np
 import pytest
@@ -594,3 +596,52 @@ def test_msm_fused_histogram_sort_2p24(gpu_programs, cname, cid, tmp_path):
     got = np.array([int(x, 16) for x in res.stdout.split()], dtype=np.uint64)
     kat = co.kat_scalar(cid, a, b, E, nthreads=16)
     assert same_point(cid, got, co.gen_mul(cid, kat))
+
+
+_BOUNDARY_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import ecgpu
+cname, path_b, path_e = sys.argv[2], sys.argv[3], sys.argv[4]
+B, E = np.load(path_b), np.load(path_e)
+prog = ecgpu.program(ecgpu.Device(0))
+n = E.shape[0]
+d_b = ecgpu.DeviceBuffer.upload(prog, B)
+d_e = ecgpu.DeviceBuffer.upload(prog, E)
+outs = [ecgpu.msm_dev(prog, cname, d_b, d_e, n)]
+outs += [ecgpu.msm_grid_part(prog, cname, d_b, d_e, n, r, 3)[0] for r in range(3)]
+for o in outs:
+    print(" ".join("%x" % int(v) for v in o))
+"""
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_boundary_form_pipeline(gpu_programs, cname, cid, tmp_path):
+    """ECG_MSM_RR=0 (the boundary-form bucket pipeline, a documented A/B knob)
+    in a child process: a single MSM and the three grid parts of a 3-rank split
+    must equal multiexp_cpu.  Its window sums stay in device memory, not in the
+    mapped host buffer the reduced-radix pipeline writes (the host
+    fold once read that buffer unconditionally)."""
+    import subprocess
+
+    cv = po.CURVES[cname]
+    n = 5003
+    B = co.gen_bases(cid, 71, 73, n, 16)
+    E = rand_scalars_np(cv, n, 4711 + cid)
+    want = co.multiexp_cpu(cid, B, E, nthreads=16)
+    pb, pe = str(tmp_path / "b.npy"), str(tmp_path / "e.npy")
+    np.save(pb, B)
+    np.save(pe, E)
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "0g-ec-gpu_amd")
+    res = subprocess.run([sys.executable, "-c", _BOUNDARY_CHILD, pkg, cname, pb, pe],
+                         env=dict(os.environ, ECG_MSM_RR="0"), capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stderr[-2000:]
+    outs = [np.array([int(x, 16) for x in ln.split()], dtype=np.uint64) for ln in res.stdout.split("\n") if ln.strip()]
+    assert len(outs) == 4
+    assert same_point(cid, outs[0], want)
+    nq = ecgpu.CURVE_FQ_LIMBS[cid]
+    acc = np.zeros(3 * nq, dtype=np.uint64)
+    for p in outs[1:]:
+        co.lib().orc_jac_add(cid, co.ptr(acc), co.ptr(acc), co.ptr(np.ascontiguousarray(p)))
+    assert same_point(cid, acc, want)
