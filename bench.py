@@ -777,6 +777,14 @@ def main():
         ecgpu.ec_fft_dev(prog, g2, d_j2, om_2, l2)
         aux["g2_ec_fft"] = {"log_n": l2, "ms": (time.perf_counter() - t_a) * 1e3}
         d_j2.free()
+        # the reference's ag-cuda-ec benches with their own checks, on this curve and (default
+        # run) on BN254, the curve those benches compile for (ag-cuda-ec/Cargo.toml:36)
+        dev_index = 0 if args.single_device else local_rank
+        for key, cv in (("reference_benches", args.curve),) + ((("reference_benches_bn254", "bn254"),) if cid == 0 else ()):
+            try:
+                aux[key] = reference_bench_suite(prog, cv, dev_index, nthreads, co20)
+            except Exception as e:  # a side line must not sink the headline line
+                aux[key] = {"error": f"{type(e).__name__}: {e}"}
 
     if rank != 0:
         group.barrier()
@@ -874,6 +882,152 @@ def main():
     print(json.dumps(line))
     group.barrier()
     group.close()
+
+
+def _fold_points(co, cid: int, pts: np.ndarray) -> np.ndarray:
+    """sum of normalised Jacobian points on the host (checker only)."""
+    lq = ecgpu.CURVE_FQ_LIMBS[cid]
+    acc = np.zeros(3 * lq, dtype=np.uint64)
+    for p in np.asarray(pts, dtype=np.uint64).reshape(-1, 3 * lq):
+        co.lib().orc_jac_add(cid, co.ptr(acc), co.ptr(acc), co.ptr(np.ascontiguousarray(p)))
+    return acc
+
+
+def _same_point(co, cid: int, a: np.ndarray, b: np.ndarray) -> bool:
+    x, y = co.jac_to_affine(cid, a), co.jac_to_affine(cid, b)
+    return (x is None and y is None) or (x is not None and y is not None and bool((x == y).all()))
+
+
+def reference_bench_suite(prog, curve: str, dev_index: int, nthreads: int, co) -> dict:
+    """The reference's own ag-cuda-ec benches on `curve`, each with the check
+    the bench itself makes (ag-cuda-ec compiles them for BN254 by default,
+    Cargo.toml:36 + pairing_suite.rs:1-12):
+      * benches/multiexp.rs:15-62: 2^22 terms (bases cycled with period 99,
+        scalars with period 73), multiple_multiexp_st(.., 1024, 8, false);
+        check: the sum of the 1024 task results == the CPU MSM of all terms;
+      * benches/amt.rs:14-56: 10 lines of 2^21 bases (period 97), one row of
+        2^21 scalars (period 73), group degrees 7..11 (window sizes 4..9 are
+        the reference kernel's knobs; this engine picks its own window, so one
+        timing per group degree); check: every group degree's task results sum
+        to the same per-line points, and line 0 equals the CPU MSM;
+      * benches/ec_fft.rs:20-55: one radix_ec_fft per degree 0..11 on host
+        points, checked against serial_ec_fft;
+      * benches/ec_fft.rs:62-112: 32 concurrent tasks of a forward + inverse
+        2^6 transform on their own contexts; check: output = n x input.
+    Timings are best of 3 after one warm call (the reference prints one)."""
+    import threading
+
+    cid = ecgpu.CURVE_NAMES[curve]
+    lq = ecgpu.CURVE_FQ_LIMBS[cid]
+    r_int = R_BLS if cid == 0 else R_BN
+    out = {"curve": curve}
+
+    def best_of(fn, k=3):
+        fn()
+        b = 1e9
+        for _ in range(k):
+            t = time.perf_counter()
+            fn()
+            b = min(b, time.perf_counter() - t)
+        return b
+
+    # ---- benches/multiexp.rs
+    n = 1 << 22
+    hb = np.ascontiguousarray(np.resize(co.gen_bases(cid, 41, 43, 99), (n, 2 * lq)))
+    he = np.ascontiguousarray(np.resize(rand_scalars(np.random.default_rng(73), 73, r_int), (n, 4)))
+    d_b = ecgpu.upload_multiexp_bases(prog, hb, curve=curve)
+    d_e = ecgpu.DeviceBuffer.upload(prog, he)
+    res = {}
+
+    def mm():
+        res["o"] = ecgpu.multiple_multiexp(prog, d_b, (d_e, n), 1024, 8, False, curve=curve)
+
+    s = best_of(mm)
+    want = co.multiexp_cpu(cid, hb, he, nthreads=nthreads)
+    out["multiexp"] = {"shape": "2^22 terms (bases period 99, scalars period 73), 1024 tasks of 4096, window 8",
+                       "ms": s * 1e3, "terms_per_s": n / s,
+                       "equal": _same_point(co, cid, _fold_points(co, cid, res["o"]), want)}
+    d_b.free()
+    d_e.free()
+    del hb, he
+    # ---- benches/amt.rs
+    L, lines = 1 << 21, 10
+    hb = np.ascontiguousarray(np.resize(co.gen_bases(cid, 7, 11, 97), (L * lines, 2 * lq)))
+    he = np.ascontiguousarray(np.resize(rand_scalars(np.random.default_rng(173), 73, r_int), (L, 4)))
+    d_b = ecgpu.upload_multiexp_bases(prog, hb, curve=curve)
+    d_e = ecgpu.DeviceBuffer.upload(prog, he)
+    sweep, line_sums = {}, None
+    equal = True
+    for gd in range(7, 12):
+        groups = 1 << gd
+
+        def amt():
+            res["o"] = ecgpu.multiple_multiexp(prog, d_b, (d_e, L), groups, 8, True, curve=curve)
+
+        sweep[str(gd)] = best_of(amt) * 1e3
+        sums = [_fold_points(co, cid, res["o"][ln * groups:(ln + 1) * groups]) for ln in range(lines)]
+        if line_sums is None:
+            line_sums = sums
+            equal = equal and _same_point(co, cid, sums[0], co.multiexp_cpu(cid, hb[:L], he, nthreads=nthreads))
+        else:
+            equal = equal and all(_same_point(co, cid, a, b) for a, b in zip(sums, line_sums))
+    out["amt"] = {"shape": f"{lines} lines x 2^21 terms (bases period 97, scalars period 73)",
+                  "ms_by_group_degree": sweep, "terms_per_s_best": L * lines / (min(sweep.values()) / 1e3),
+                  "equal": bool(equal)}
+    d_b.free()
+    d_e.free()
+    del hb, he
+    # ---- benches/ec_fft.rs (sequential): radix_ec_fft per degree 0..11, host points
+    p_mod = P_BLS if cid == 0 else P_BN
+    one = u64(((1 << (64 * lq)) % p_mod), lq)
+    aff = co.gen_bases(cid, 3, 7, 1 << 11)
+    jac = np.ascontiguousarray(np.concatenate([aff, np.tile(one, (1 << 11, 1))], axis=1))
+    ek = ecgpu.EcFftKernel.create([prog], curve)
+    seq, eq_seq = {}, True
+    for deg in range(12):
+        x = np.ascontiguousarray(jac[:1 << deg])
+        om = omega_for(cid, r_int, deg)
+
+        def one_fft():
+            y = x.copy()
+            ek.radix_ec_fft(y, om, deg)
+            res["o"] = y
+
+        seq[str(deg)] = best_of(one_fft) * 1e3
+        ref = co.serial_ec_fft(cid, x, om, deg, nthreads=nthreads)
+        eq_seq = eq_seq and all(_same_point(co, cid, a, b) for a, b in zip(res["o"], ref))
+    out["ec_fft_sequential"] = {"ms_by_log_n": seq, "equal": bool(eq_seq)}
+    # ---- benches/ec_fft.rs (parallel): 32 threads, forward + inverse 2^6 each on its own context
+    ln6, tasks = 6, 32
+    om6 = omega_for(cid, r_int, ln6)
+    w6 = int(sum(int(v) << (64 * i) for i, v in enumerate(om6))) * pow(1 << 256, -1, r_int) % r_int
+    om6_inv = u64(pow(w6, -1, r_int) * (1 << 256) % r_int)
+    tprogs = [ecgpu.program(ecgpu.Device(dev_index)) for _ in range(tasks)]
+    tks = [ecgpu.EcFftKernel.create([tp], curve) for tp in tprogs]
+    xs = [np.ascontiguousarray(jac[(i % 32) << ln6:((i % 32) + 1) << ln6]) for i in range(tasks)]
+
+    def par_round():
+        ys = [x.copy() for x in xs]
+
+        def task(i):
+            tks[i].radix_ec_fft(ys[i], om6, ln6)
+            tks[i].radix_ec_fft(ys[i], om6_inv, ln6)
+
+        th = [threading.Thread(target=task, args=(i,)) for i in range(tasks)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        res["o"] = ys
+
+    ps = best_of(par_round)
+    n6 = co.u64arr([1 << ln6], 4)
+    ok = all(_same_point(co, cid, res["o"][i][j], co.naive_multiexp(cid, np.ascontiguousarray(xs[i][j:j + 1, :2 * lq]), n6))
+             for i in (0, tasks - 1) for j in range(1 << ln6))
+    for tp in tprogs:
+        tp.close()
+    out["ec_fft_parallel"] = {"tasks": tasks, "log_n": ln6, "ms": ps * 1e3, "forward_inverse_is_n_times_input": bool(ok)}
+    return out
 
 
 def _g2_kat(cid: int, scal: np.ndarray, r_int: int, got: np.ndarray) -> bool:

@@ -48,6 +48,7 @@ def lib():
             "orc_pow_u64": (None, [i, _u64p, _u64p, u64]),
             "orc_serial_fft": (None, [i, _u64p, _u64p, u32]),
             "orc_parallel_fft": (i, [i, _u64p, _u64p, u32, u32]),
+            "orc_poly_eval": (None, [i, _u64p, sz, _u64p, _u64p]),
             "orc_multiexp_cpu": (i, [i, _u64p, _u64p, sz, _u64p, i, u32]),
             "orc_naive_multiexp": (None, [i, _u64p, _u64p, sz, _u64p]),
             "orc_jac_double": (None, [i, _u64p, _u64p]),
@@ -120,6 +121,14 @@ def parallel_fft(fid: int, a: np.ndarray, omega: np.ndarray, log_n: int, log_thr
     if rc != 0:
         raise ValueError("parallel_fft failed: %d" % rc)
     return a
+
+
+def poly_eval(fid: int, a: np.ndarray, x: np.ndarray) -> np.ndarray:
+    """sum_j a_j x^j (Montgomery in and out): one DFT output X_k = P(omega^k)."""
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    out = np.zeros(limbs(fid), dtype=np.uint64)
+    lib().orc_poly_eval(fid, ptr(a), a.shape[0], ptr(np.ascontiguousarray(x, dtype=np.uint64)), ptr(out))
+    return out
 
 
 class IdentityBaseError(ValueError):

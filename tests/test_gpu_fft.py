@@ -161,3 +161,61 @@ def test_fft_errors_and_abort(kernels, gpu_programs):
     ka = ecgpu.FftKernel.create_with_abort(progs, lambda: True)
     with pytest.raises(ecgpu.Aborted):
         ka.radix_fft(np.zeros((16, 4), np.uint64), om, 4)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("fname,fid,log_n", [("bls12_381_fr", 0, 26), ("bn254_fr", 2, 28)])
+def test_fft_large_matches_parallel_fft(kernels, fname, fid, log_n):
+    """Sizes above 2^24 up to BN254's two-adicity (fft.rs:14,80-87 accepts up
+    to LOG2_MAX_ELEMENTS): 2^26 BLS12-381 Fr (passes of 9/9/8) and 2^28 BN254
+    Fr (10/9/9, the largest transform with full per-pass twiddle tables and
+    64-bit element indices past 2^31 bytes), bit-exact vs CPU parallel_fft."""
+    f = po.FIELDS[fname]
+    a = rand_mont(f, 1 << log_n, 100 + log_n)
+    om = co.u64arr([f.to_mont(f.omega(1 << log_n))], 4)[0]
+    ref = co.parallel_fft(fid, a, om, log_n, 4)
+    kernels[fname].radix_fft(a, om, log_n)
+    assert (a == ref).all()
+
+
+@pytest.mark.timeout(600)
+def test_fft_2p29_spots_and_round_trip(kernels):
+    """2^29 BLS12-381 Fr: above 2^28 the passes run on the split twiddle
+    tables (no full per-pass tables, 32-bit-limb butterflies).  Too large for
+    the CPU FFT in a test, so: two outputs against their definition
+    X_k = sum_j a_j w^(jk) (oracle poly_eval), and FFT(w^-1) o FFT(w) = n id
+    on 512 sampled rows."""
+    f = po.BLS12_381_FR
+    log_n = 29
+    n = 1 << log_n
+    a = rand_mont(f, n, 29)
+    w = f.omega(n)
+    om = co.u64arr([f.to_mont(w)], 4)[0]
+    om_inv = co.u64arr([f.to_mont(pow(w, -1, f.modulus))], 4)[0]
+    k = kernels["bls12_381_fr"]
+    b = a.copy()
+    k.radix_fft(b, om, log_n)
+    for kk in (1, n // 2 + 12345):
+        x = co.u64arr([f.to_mont(pow(w, kk, f.modulus))], 4)[0]
+        assert (co.poly_eval(0, a, x) == b[kk]).all(), kk
+    k.radix_fft(b, om_inv, log_n)
+    for i in np.random.default_rng(1).integers(0, n, size=512):
+        x = f.from_mont(co.to_ints(a[i:i + 1])[0])
+        y = f.from_mont(co.to_ints(b[i:i + 1])[0])
+        assert y == x * n % f.modulus
+
+
+@pytest.mark.timeout(300)
+def test_fft_many_with_2p25_among_small(kernels):
+    """radix_fft_many (fft.rs:211-246) with a 2^25 input between small ones of
+    other sizes and omegas: every output equals its own CPU FFT."""
+    f = po.BLS12_381_FR
+    sizes = [10, 25, 3, 12, 10]
+    ins = [rand_mont(f, 1 << s, 250 + j) for j, s in enumerate(sizes)]
+    oms = [co.u64arr([f.to_mont(pow(f.omega(1 << s), 1 + 2 * j, f.modulus))], 4)[0] for j, s in enumerate(sizes)]
+    refs = [co.serial_fft(0, a, om, s) if s <= 12 else co.parallel_fft(0, a, om, s, 4)
+            for a, om, s in zip(ins, oms, sizes)]
+    outs = [a.copy() for a in ins]
+    kernels["bls12_381_fr"].radix_fft_many(outs, oms, sizes)
+    for o, r, s in zip(outs, refs, sizes):
+        assert (o == r).all(), s

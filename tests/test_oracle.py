@@ -102,6 +102,22 @@ def test_fft_known_answers():
     assert (co.serial_fft(0, ones, om, log_n) == want).all()            # DFT(1) = n delta_0
 
 
+@pytest.mark.parametrize("fname", ["bls12_381_fr", "bn254_fr"])
+def test_poly_eval_is_one_dft_output(fname):
+    """poly_eval (the spot check of GPU transforms too large for the CPU FFT)
+    returns X_k of serial_fft's output for every k of a 2^9 transform."""
+    f = po.FIELDS[fname]
+    fid = co.FIELD_IDS[fname]
+    n = 1 << 9
+    rng = po.Xoshiro256ss(77)
+    a = co.u64arr([f.to_mont(rng.field_element(f)) for _ in range(n)], 4)
+    w = f.omega(n)
+    ref = co.serial_fft(fid, a, co.u64arr([f.to_mont(w)], 4)[0], 9)
+    for k in range(n):
+        x = co.u64arr([f.to_mont(pow(w, k, f.modulus))], 4)[0]
+        assert (co.poly_eval(fid, a, x) == ref[k]).all(), k
+
+
 def test_config1_serial_fft_2p16_hash():
     """BASELINE config (1): BLS12-381 Fr FFT 2^16 on serial_fft -- C restatement
     reproduces the Python restatement's output hash."""

@@ -81,7 +81,7 @@ case $cmd in
   round)
     TAG=$1
     tests && bench && {
-      timeout -k 10 600 python3 bench.py --curve bn254 --no-e2e --no-aux > $R/gpurun_out/bench_bn254.log 2>&1; rc=$?
+      timeout -k 10 600 python3 bench.py --curve bn254 --no-e2e > $R/gpurun_out/bench_bn254.log 2>&1; rc=$?
       echo "bn254 bench rc=$rc"; [ $rc -eq 0 ]; } && prof $TAG ;;
   *) echo "unknown subcommand $cmd"; exit 2 ;;
 esac
