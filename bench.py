@@ -248,11 +248,16 @@ def launch_ranks(n: int, argv=None, grace_s: float = 60.0) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(sys.argv[0]), *argv], env=env,
                                       start_new_session=True))
     rc, first_fail = 0, None
+    t_start = t_beat = time.monotonic()
     try:
         while True:
             codes = [p.poll() for p in procs]
             if all(c is not None for c in codes):
                 break
+            if time.monotonic() - t_beat > 30:  # a heartbeat: the ranks print only at the end
+                t_beat = time.monotonic()
+                print(f"bench: {sum(c is None for c in codes)} of {n} ranks running, "
+                      f"{t_beat - t_start:.0f} s", file=sys.stderr, flush=True)
             failed = [c for c in codes if c not in (None, 0)]
             if failed and first_fail is None:
                 first_fail = time.monotonic()

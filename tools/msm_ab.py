@@ -1,4 +1,5 @@
-"""A/B of MSM tunables (env vars read once per process -> one subprocess per
+"""A/B of MSM tunables (AB_CURVE=bn254 for the other G1 curve; ECGPU_LIB=<lib> as a config
+selects another in-tree build) (env vars read once per process -> one subprocess per
 config, interleaved rounds).  Dev tool: prints per-kernel times from the
 library's HIP-event timer and the end-to-end ms per 2^N MSM."""
 import os, subprocess, sys, json
@@ -14,15 +15,16 @@ n = 1 << %d
 rng = np.random.default_rng(7)
 E = rng.integers(0, 2**64, size=(n, 4), dtype=np.uint64); E[:, 3] &= np.uint64(2**62 - 1)
 d_e = ecgpu.DeviceBuffer.upload(prog, E)
-d_b = ecgpu.gen_bases_dev(prog, "bls12_381", 12345, 678910, n)
-for _ in range(2): ecgpu.msm_dev(prog, "bls12_381", d_b, d_e, n)
+CV = "%s"
+d_b = ecgpu.prepare_bases(prog, CV, ecgpu.gen_bases_dev(prog, CV, 12345, 678910, n), n)
+for _ in range(2): ecgpu.msm_dev(prog, CV, d_b, d_e, n)
 best = 1e9; acc = 1e9
 for _ in range(5):
-    t = time.perf_counter(); out = ecgpu.msm_dev(prog, "bls12_381", d_b, d_e, n); best = min(best, time.perf_counter() - t)
+    t = time.perf_counter(); out = ecgpu.msm_dev(prog, CV, d_b, d_e, n); best = min(best, time.perf_counter() - t)
     acc = min(acc, prog.kernel_time("msm_accumulate")[0])
 import hashlib
 print(json.dumps({"ms": best * 1e3, "acc_ms": acc, "result": hashlib.sha256(out.tobytes()).hexdigest()[:16]}))
-''' % (ROOT, LOG)
+''' % (ROOT, LOG, os.environ.get("AB_CURVE", "bls12_381"))
 for rnd in range(2):
     for cfg in CONFIGS:
         env = dict(os.environ, **cfg)
