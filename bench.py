@@ -827,10 +827,11 @@ def main():
                                            "note": f"{MAD_ISSUE_CYCLES} SIMD cycles per wave64 v_mad_u64_u32 "
                                                    "(tools/issue_bench.hip) at 2.4 GHz"},
                          "mads_per_add": mads, "mixed_adds_per_s": n_acc * W / (acc_avg_ms / 1e3),
-                         "note": f"{mads} v_mad_u64_u32 per XYZZ mixed add (8M+2S, {RR_LIMBS[cid]} x {RR_BITS[cid]}-bit limbs; "
-                                 "BLS12-381's 13 x 30-bit layout issues 14 % fewer mads per add than round 4's 14 x 29 "
-                                 "bits, so this fraction is lower while mixed_adds_per_s is higher) "
-                                 f"x {W} windows x terms / launch time; peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz"})
+                         "note": f"{mads} v_mad_u64_u32 per XYZZ mixed add (8M+2S, {RR_LIMBS[cid]} x {RR_BITS[cid]}-bit limbs"
+                                 + ("; BLS12-381's 13 x 30-bit layout issues 14 % fewer mads per add than round 4's "
+                                    "14 x 29 bits, so this fraction is lower while mixed_adds_per_s is higher" if cid == 0
+                                    else "; BN254's tight-slack 9 x 29-bit layout: 2117 VALU per add, 1467 of them mads")
+                                 + f") x {W} windows x terms / launch time; peak = 256 CU x 4 SIMD x 16 lanes x 2.4 GHz"})
     roofline["hbm"] = {"achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": hbm_achieved / HBM_PEAK_GBS,
                        "note": f"algorithmic {bytes_per_term} B/term ({2 * lq * 8} B base + 32 B scalar) x terms "
