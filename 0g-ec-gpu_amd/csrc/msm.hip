@@ -1,7 +1,9 @@
 // curve_id dispatch of the MSM drivers.  The per-curve kernels and drivers
 // (msm_impl.hpp) are compiled once per curve in msm_inst.hip (-DECG_INST=id),
 // which exports one MsmOps table each; this file only routes calls.
+#include <algorithm>
 #include <atomic>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -269,12 +271,31 @@ int msm_grid_run(ecg_ctx* ctx, int curve_id, const void* d_bases, const void* d_
         if (pieces) *pieces = 0;
         return o->point_sum(nullptr, 0, out_jac);
       }
-      const uint32_t w0 = (uint32_t)(a / n), wl = (uint32_t)((b - 1) / n);
-      if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144, per device pass
-      ECG_TRY(o->grid(ctx, d_bases, d_scalars, n, w0, wl - w0 + 1, (size_t)(a - (uint64_t)w0 * n),
-                      (size_t)(b - (uint64_t)wl * n), out_jac, s, f));
-      if (pieces) *pieces = 1;
-      return ECG_OK;
+      // Entries one device pass may hold: the terms per pass of a whole MSM (msm_pass_terms,
+      // calc_chunk_size's memory budget, multiexp.rs:71-93) times its windows.  A larger share
+      // (huge n, or a context capped by ecg_ctx_set_mem_limit / ecg_ctx_set_msm_chunk) runs as
+      // consecutive sub-ranges of the grid, one core call each, whose partials are summed.
+      const uint64_t max_e = std::max<uint64_t>((uint64_t)o->pass_terms(ctx) * W, 1);
+      std::vector<uint64_t> parts;
+      int np = 0;
+      for (uint64_t e0 = a; e0 < b;) {
+        uint64_t e1 = std::min<uint64_t>(b, e0 + max_e);
+        const uint32_t w0 = (uint32_t)(e0 / n);
+        if ((e1 - 1) / n - w0 + 1 > 16) e1 = (uint64_t)(w0 + 16) * n;  // at most 16 window blocks per call
+        const uint32_t wl = (uint32_t)((e1 - 1) / n);
+        if (abort_cb && abort_cb(user)) return ECG_ABORTED;  // multiexp.rs:140-144, per device pass
+        parts.resize(parts.size() + 3 * lq);
+        ECG_TRY(o->grid(ctx, d_bases, d_scalars, n, w0, wl - w0 + 1, (size_t)(e0 - (uint64_t)w0 * n),
+                        (size_t)(e1 - (uint64_t)wl * n), parts.data() + parts.size() - 3 * lq, s, f));
+        np++;
+        e0 = e1;
+      }
+      if (pieces) *pieces = np;
+      if (np == 1) {
+        memcpy(out_jac, parts.data(), 3 * lq * 8);
+        return ECG_OK;
+      }
+      return o->point_sum(parts.data(), (size_t)np, out_jac);
     }
     const size_t stride = f.prepared ? msm_prepared_stride(curve_id, 0) : 2 * lq * 8;
     std::vector<uint64_t> parts;

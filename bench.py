@@ -806,15 +806,18 @@ def main():
     # the committed PMC passes profile the default (BLS12-381, 2^26 / 2^24) run
     default_run = cid == 0 and args.msm_log == 26 and log_n == 24 and world == 1
     acc_traffic, acc_src = pmc_traffic("msm_accumulate") if default_run else (None, None)
-    if cid == 1 and args.msm_log == 26 and world == 1:  # BN254 (config 5): its own committed PMC pass
-        bn = os.path.join(ROOT, "profiles", "pmc_bn254_current.json")  # copy of profiles/r05/pmc_bn254_accumulate.json
+    ntt_traffic, ntt_src = pmc_traffic("ntt_pass") if default_run else (None, None)
+    if cid == 1 and world == 1:  # BN254 (config 5): its own committed PMC passes
+        bn = os.path.join(ROOT, "profiles", "pmc_bn254_current.json")
         try:
             with open(bn) as f:
                 d_bn = json.load(f)
-            acc_traffic, acc_src = d_bn["traffic_gb_per_launch"], d_bn["source"]
+            if args.msm_log == 26:
+                acc_traffic, acc_src = d_bn["traffic_gb_per_launch"], d_bn["source"]
+            if log_n == 24 and "ntt_traffic_gb_per_launch" in d_bn:
+                ntt_traffic, ntt_src = d_bn["ntt_traffic_gb_per_launch"], d_bn["ntt_source"]
         except (OSError, ValueError, KeyError, TypeError) as e:
             print(f"bench: ignoring {bn}: {type(e).__name__}: {e}", file=sys.stderr)
-    ntt_traffic, ntt_src = pmc_traffic("ntt_pass") if default_run else (None, None)
     ntt_achieved = 64 * n_ntt / (pass_avg_ms / 1e3) / 1e9
     roofline = {"bound": "valu", "kernel": "msm_accumulate", "avg_ms": acc_avg_ms,
                 "traffic": acc_traffic, "traffic_unit": "GB/launch", "traffic_source": acc_src}

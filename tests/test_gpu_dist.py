@@ -457,6 +457,36 @@ def test_msm_grid_parts(gpu_programs, cname, cid, prepared):
             d_e.free()
 
 
+@pytest.mark.parametrize("cname,cid", [("bls12_381", 0), ("bn254", 1)])
+def test_msm_grid_part_chunked_by_pass_budget(gpu_programs, cname, cid):
+    """A grid share larger than one device pass (here: the context pinned to
+    2^9-term passes, ecg_ctx_set_msm_chunk) runs as several one-call
+    sub-ranges whose partials are summed: the ranks' partials
+    still fold to multiexp_cpu, and a share reports more than one piece."""
+    prog = ecgpu.program(gpu_programs[1][0])
+    cv = po.CURVES[cname]
+    n = 5003
+    B = co.gen_bases(cid, 41, 47, n, 8)
+    E = rand_fr(cv.fr, n, 90 + cid)
+    want = co.jac_to_affine(cid, co.multiexp_cpu(cid, B, E, nthreads=8))
+    d_b = ecgpu.DeviceBuffer.upload(prog, B)
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    try:
+        prog.set_msm_chunk(1 << 9)
+        for nranks in (3, 5):
+            parts, pieces = [], []
+            for r in range(nranks):
+                p, k = ecgpu.msm_grid_part(prog, cname, d_b, d_e, n, r, nranks)
+                parts.append(p)
+                pieces.append(k)
+            assert max(pieces) > 1, pieces
+            assert (co.jac_to_affine(cid, _fold_parts(cid, parts)) == want).all(), nranks
+    finally:
+        d_b.free()
+        d_e.free()
+        prog.close()
+
+
 def test_msm_grid_part_rejects(gpu_programs):
     """Bad rank numbers and window-table bases are refused, not run."""
     prog = gpu_programs[0][0]

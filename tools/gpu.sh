@@ -72,12 +72,22 @@ diag() {
   pmc ${TAG}_sq2_ntt "$SQ2" $R/tools/ntt_once.py 24 3
 }
 
+# BN254 counter passes (bench line's BN254 roofline.traffic): accumulate at 2^26, NTT at 2^24
+bnpmc() {
+  local TAG=$1
+  pmc ${TAG}_bn_acc_fetch "FETCH_SIZE" $R/tools/msm_once.py 26 1 1 bn254 &&
+  pmc ${TAG}_bn_acc_write "WRITE_SIZE" $R/tools/msm_once.py 26 1 1 bn254 &&
+  pmc ${TAG}_bn_ntt_fetch "FETCH_SIZE" $R/tools/ntt_once.py 24 3 bn254_fr &&
+  pmc ${TAG}_bn_ntt_write "WRITE_SIZE" $R/tools/ntt_once.py 24 3 bn254_fr
+}
+
 case $cmd in
   tests) tests "$@" ;;
   bench) bench "$@" ;;
   prof) prof "$@" ;;
   sq) sq "$@" ;;
   diag) diag "$@" ;;
+  bnpmc) bnpmc "$@" ;;
   round)
     TAG=$1
     tests && bench && {
