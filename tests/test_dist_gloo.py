@@ -407,6 +407,7 @@ def test_bench_reads_committed_pmc_records():
     with open(os.path.join(ROOT, "profiles", "pmc_bn254_current.json")) as f:
         d = json.load(f)
     assert d["traffic_gb_per_launch"] > 0 and d["source"].startswith("profiles/")
+    assert d["ntt_traffic_gb_per_launch"] > 0 and d["ntt_source"].startswith("profiles/")
 
 
 def _gloo_worker(rank, world, port, q):
