@@ -240,3 +240,56 @@ def test_prepared_registry_across_contexts_and_views(prog):
     for buf in (d_b, d_e, d_e2):
         buf.free()
     other.close()
+
+
+def test_stale_entry_refused_call_confirms_header(prog):
+    """a call that the registry would refuse -- more bases than a
+    prepared entry holds, or a window-table entry in the grid split -- first
+    checks the entry's header on the stream.  When another owner has
+    overwritten the allocation with raw [x, y] bases, the entry is dropped and
+    the call runs over the raw bases (same result as multiexp_cpu) instead of
+    being refused now and at every later call."""
+    cid, cname = 0, "bls12_381"
+    cv = po.CURVES[cname]
+    n = 3000
+    hdr = 256  # msm.hip PREP_HEADER
+    hip = ctypes.CDLL(ecgpu.lib().ecg_runtime_info().decode().split("(")[1].split(")")[0])
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    m = n * 4 // 3  # raw [x, y] bases (96 B) that fit in n prepared 128-B records
+    B = co.gen_bases(cid, 71, 73, m, 8)
+    E = rand_scalars(cv, m, 75)
+    d_b = ecgpu.DeviceBuffer.upload(prog, B[:n])
+    d_e = ecgpu.DeviceBuffer.upload(prog, E)
+    raw = np.ascontiguousarray(np.concatenate([np.zeros(hdr // 8, np.uint64), B.reshape(-1)]))
+
+    def overwrite(pb):
+        prog.synchronize()
+        assert hip.hipMemcpy(ctypes.c_void_p(pb.ptr.value - hdr), raw.ctypes.data_as(ctypes.c_void_p), raw.nbytes, 1) == 0
+        return ecgpu.PreparedBases(prog, ctypes.c_void_p(pb.ptr.value), cid, m)
+
+    try:
+        # a plain prepared entry of n records, read as m > n raw bases
+        pb = ecgpu.prepare_bases(prog, cname, d_b, n)
+        view = overwrite(pb)
+        want = co.multiexp_cpu(cid, B, E, nthreads=8)
+        for _ in range(2):  # the second call finds no entry
+            out = np.zeros(18, np.uint64)
+            ecgpu._check(ecgpu.lib().ecg_msm_dev(prog.handle, cid, view.ptr, d_e.ptr, m,
+                                                 out.ctypes.data_as(ctypes.c_void_p), 0, None))
+            assert same(cid, out, want)
+        view.ptr = None
+        assert hip.hipFree(ctypes.c_void_p(pb.ptr.value - hdr)) == 0
+        pb.ptr = None
+        # a window-table entry in the grid split (which refuses tables): its allocation holds the
+        # table's W rows per base, plenty for the raw bases
+        tb = ecgpu.prepare_bases(prog, cname, d_b, n, window_table=8)
+        view = overwrite(tb)
+        part, _ = ecgpu.msm_grid_part(prog, cname, view, d_e, n, 0, 1)
+        assert same(cid, part, co.multiexp_cpu(cid, B[:n], E[:n], nthreads=8))
+        view.ptr = None
+        assert hip.hipFree(ctypes.c_void_p(tb.ptr.value - hdr)) == 0
+        tb.ptr = None
+    finally:
+        d_b.free()
+        d_e.free()
