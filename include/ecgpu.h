@@ -392,7 +392,11 @@ int ecg_msm_dist_ex(ecg_ctx *ctx, int curve_id, const void *d_bases, const void 
  * width), so every rank does the same bucket work whatever n and nranks are.
  * Partials and statuses are exchanged and folded as in ecg_msm_dist; the
  * result is bit-identical to ecg_msm over the n terms.  Bases may be a
- * prepared buffer (ecg_msm_prepare) or [x, y] records, not a window table. */
+ * prepared buffer (ecg_msm_prepare) or [x, y] records, not a window table.
+ * Every rank must pass the same n: n rides in the status record, and ranks
+ * called with different sizes all return ECG_ERR_INVALID.  A share larger
+ * than one device pass (the context's memory budget, ecg_ctx_set_mem_limit /
+ * ecg_ctx_set_msm_chunk) runs as several passes. */
 int ecg_msm_dist_grid(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n,
                       uint64_t *out_jac);
 int ecg_msm_dist_grid_ex(ecg_ctx *ctx, int curve_id, const void *d_bases, const void *d_scalars, size_t n,
