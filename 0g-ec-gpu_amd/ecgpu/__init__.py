@@ -97,6 +97,8 @@ _SIGS = {
     "ecg_point_sum_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, _u64p,
                                          ctypes.c_void_p]),
     "ecg_point_sum": (ctypes.c_int, [ctypes.c_int, _u64p, ctypes.c_size_t, _u64p]),
+    "ecg_field_ops": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _u64p, _u64p,
+                                     ctypes.c_uint32, ctypes.c_size_t, _u64p]),
     "ecg_ec_fft": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, _u64p, _u64p, ctypes.c_uint32, ABORT_CB,
                                   ctypes.c_void_p]),
     "ecg_ec_fft_many": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int,
@@ -436,6 +438,24 @@ def msm_dev(prog: Program, curve, d_bases: DeviceBuffer, d_scalars: DeviceBuffer
     out = np.zeros(3 * CURVE_FQ_LIMBS[cid], dtype=np.uint64)
     _check(lib().ecg_msm_dev(prog.handle, cid, d_bases.ptr, d_scalars.ptr, n,
                              out.ctypes.data_as(ctypes.c_void_p), 0, None), "msm_dev")
+    return out
+
+
+FOP_ADD, FOP_SUB, FOP_MUL, FOP_SQR, FOP_DOUBLE, FOP_POW, FOP_MONT, FOP_UNMONT, FOP_INV = range(9)
+
+
+def field_ops(prog: Program, field, form: int, op: int, a: np.ndarray, b: np.ndarray | None = None,
+              e: int = 0) -> np.ndarray:
+    """ecg_field_ops: one field operation element-wise on the device in one of
+    the engine's field forms (0 boundary, 1 product-path reduced radix, 2 an
+    Fq's G2 reduced radix) -- the reference's GPU field tests
+    (ag-build/src/tests/test_fields.rs).  a, b: (n, limbs) u64 Montgomery."""
+    fid = FIELD_NAMES[field] if isinstance(field, str) else int(field)
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    bb = None if b is None else np.ascontiguousarray(b, dtype=np.uint64)
+    out = np.zeros_like(a)
+    _check(lib().ecg_field_ops(prog.handle, fid, form, op, _ptr(a), _ptr(bb) if bb is not None else None, int(e),
+                               a.shape[0], _ptr(out)), "field_ops")
     return out
 
 

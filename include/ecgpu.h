@@ -303,6 +303,28 @@ size_t ecg_base_cache_keys(ecg_ctx *ctx, const void **out, size_t cap);
 int ecg_msm_plan_info(int curve_id, size_t n, uint32_t window_bits, uint32_t *c, uint32_t *windows,
                       int *sort_mode);
 
+/* Element-wise field operations on the device, one engine field form at a
+ * time: the reference's GPU field tests (ag-build/src/tests/test_fields.rs:
+ * test_add/sub/mul/pow/sqr/double/mont/unmont over field.cl:14-392).
+ * form 0 = boundary form (field.hpp); 1 = the product path's reduced-radix
+ * form (fieldrr.hpp: Fr 9 x 29, BLS12-381 Fq 13 x 30, BN254 Fq 9 x 29);
+ * 2 = an Fq's second reduced-radix form (BLS12-381 14 x 29, BN254 10 x 28: the
+ * G2 components).  a, b, out: n elements of host memory in the field's
+ * Montgomery form (ECG_FOP_MONT takes canonical inputs, ECG_FOP_UNMONT returns
+ * them; forms 1-2 have neither); e is ECG_FOP_POW's exponent; b may be NULL
+ * for the unary ops.  Outputs are canonical (fully reduced). */
+#define ECG_FOP_ADD 0
+#define ECG_FOP_SUB 1
+#define ECG_FOP_MUL 2
+#define ECG_FOP_SQR 3
+#define ECG_FOP_DOUBLE 4
+#define ECG_FOP_POW 5
+#define ECG_FOP_MONT 6
+#define ECG_FOP_UNMONT 7
+#define ECG_FOP_INV 8
+int ecg_field_ops(ecg_ctx *ctx, int field_id, int form, int op, const uint64_t *a, const uint64_t *b, uint32_t e,
+                  size_t n, uint64_t *out);
+
 /* Sum `count` Jacobian points (3 x Lq u64 each, device memory) into one
  * normalised Jacobian point: the EC fold that follows the RCCL all-gather of
  * per-GPU partials (RCCL has no EC-add reduction op).  The points are copied

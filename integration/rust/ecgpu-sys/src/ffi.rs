@@ -41,6 +41,15 @@ pub const ECG_BASES_XY: c_int = 0;
 pub const ECG_BASES_ARK_AFFINE: c_int = 1;
 
 // ---- ecg_msm_plan_info sort modes ---------------------------------------------
+pub const ECG_FOP_ADD: c_int = 0;
+pub const ECG_FOP_SUB: c_int = 1;
+pub const ECG_FOP_MUL: c_int = 2;
+pub const ECG_FOP_SQR: c_int = 3;
+pub const ECG_FOP_DOUBLE: c_int = 4;
+pub const ECG_FOP_POW: c_int = 5;
+pub const ECG_FOP_MONT: c_int = 6;
+pub const ECG_FOP_UNMONT: c_int = 7;
+pub const ECG_FOP_INV: c_int = 8;
 pub const ECG_SORT_GLOBAL: c_int = 0;
 pub const ECG_SORT_PW_ONE: c_int = 1;
 pub const ECG_SORT_PW_BLOCK: c_int = 2;
@@ -147,6 +156,8 @@ extern "C" {
     pub fn ecg_point_sum_dev(ctx: *mut ecg_ctx, curve_id: c_int, d_points: *const c_void, count: usize,
                              out_jac: *mut u64, stream: *mut c_void) -> c_int;
     pub fn ecg_point_sum(curve_id: c_int, points: *const u64, count: usize, out_jac: *mut u64) -> c_int;
+    pub fn ecg_field_ops(ctx: *mut ecg_ctx, field_id: c_int, form: c_int, op: c_int, a: *const u64, b: *const u64,
+                         e: u32, n: usize, out: *mut u64) -> c_int;
     pub fn ecg_msm_check_bases(curve_id: c_int, bases_xy: *const u64, scalars: *const u64, n: usize) -> c_int;
 
     // ---- multi-GPU over RCCL, one process per GPU ----
