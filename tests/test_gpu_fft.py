@@ -219,3 +219,32 @@ def test_fft_many_with_2p25_among_small(kernels):
     kernels["bls12_381_fr"].radix_fft_many(outs, oms, sizes)
     for o, r, s in zip(outs, refs, sizes):
         assert (o == r).all(), s
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("log_n", [31, 32])
+def test_fft_2p31_2p32_sparse_spot_outputs(gpu_programs, log_n):
+    """2^31 and 2^32 points (68.7 / 137 GB in, the same out, on one GPU with
+    its scratch buffer: the reference's LOG2_MAX_ELEMENTS = 32, fft.rs:14):
+    element indices past 2^31 on the split twiddle tables.  The input holds 16
+    random non-zeros at random positions, so any output X_k = sum_j a_j w^(jk)
+    is cheap to compute exactly; 64 random outputs plus the ends are compared,
+    which catches a wrong index or twiddle anywhere in the 4-pass schedule."""
+    f = po.BLS12_381_FR
+    n = 1 << log_n
+    r = f.modulus
+    rng = np.random.default_rng(2000 + log_n)
+    pos = [int(p) for p in rng.choice(n, 16, replace=False)]
+    vals = [f.from_mont(co.to_ints(v[None, :])[0]) for v in rand_mont(f, 16, 2000 + log_n)]
+    a = np.zeros((n, 4), dtype=np.uint64)
+    a[pos] = co.u64arr([f.to_mont(v) for v in vals], 4)
+    w = f.omega(n)
+    prog = ecgpu.program(gpu_programs[1][0])  # its own context: 137 GB of workspace, released below
+    try:
+        ecgpu.FftKernel.create([prog], "bls12_381_fr").radix_fft(a, co.u64arr([f.to_mont(w)], 4)[0], log_n)
+    finally:
+        prog.close()
+    ks = [0, 1, n // 2, n - 1] + [int(k) for k in rng.integers(0, n, 64)]
+    for k in ks:
+        want = sum(v * pow(w, p * k % n, r) for p, v in zip(pos, vals)) % r
+        assert f.from_mont(co.to_ints(a[k:k + 1])[0]) == want, k
