@@ -915,10 +915,10 @@ def reference_bench_suite(prog, curve: str, dev_index: int, nthreads: int, co) -
         scalars with period 73), multiple_multiexp_st(.., 1024, 8, false);
         check: the sum of the 1024 task results == the CPU MSM of all terms;
       * benches/amt.rs:14-56: 10 lines of 2^21 bases (period 97), one row of
-        2^21 scalars (period 73), group degrees 7..11 (window sizes 4..9 are
-        the reference kernel's knobs; this engine picks its own window, so one
-        timing per group degree); check: every group degree's task results sum
-        to the same per-line points, and line 0 equals the CPU MSM;
+        2^21 scalars (period 73), group degrees 7..11 with the engine's own
+        window, then the bench's whole grid (group degree 7..11 x window size
+        4..9, the window pinned); check: every run's task results sum to the
+        same per-line points, and line 0 equals the CPU MSM;
       * benches/ec_fft.rs:20-55: one radix_ec_fft per degree 0..11 on host
         points, checked against serial_ec_fft;
       * benches/ec_fft.rs:62-112: 32 concurrent tasks of a forward + inverse
@@ -983,6 +983,24 @@ def reference_bench_suite(prog, curve: str, dev_index: int, nthreads: int, co) -
     out["amt"] = {"shape": f"{lines} lines x 2^21 terms (bases period 97, scalars period 73)",
                   "ms_by_group_degree": sweep, "terms_per_s_best": L * lines / (min(sweep.values()) / 1e3),
                   "equal": bool(equal)}
+    # the bench's full grid (amt.rs:38-56): every group degree x window size
+    # 4..9, the window pinned as the reference kernel takes it (pin_window)
+    grid, eq_grid = {}, True
+    for gd in range(7, 12):
+        groups = 1 << gd
+        row = {}
+        for ws in range(4, 10):
+            def amt_w():
+                res["o"] = ecgpu.multiple_multiexp(prog, d_b, (d_e, L), groups, ws, True, curve=curve,
+                                                   pin_window=True)
+
+            row[str(ws)] = best_of(amt_w, 1) * 1e3
+            sums = [_fold_points(co, cid, res["o"][ln * groups:(ln + 1) * groups]) for ln in range(lines)]
+            eq_grid = eq_grid and all(_same_point(co, cid, a, b) for a, b in zip(sums, line_sums))
+        grid[str(gd)] = row
+    out["amt_window_grid"] = {"ms_by_group_degree_and_window": grid, "equal": bool(eq_grid),
+                              "note": "window pinned (pin_window=True) as multiple_multiexp_st(.., window_size, "
+                                      "true) takes it; each cell's per-line sums == the auto-window sweep's"}
     d_b.free()
     d_e.free()
     del hb, he
