@@ -2028,12 +2028,28 @@ double msm_term_bytes(const MsmPlan& pl) {
 }
 
 // Device memory left for an MSM's workspace: (1 - MEMORY_PADDING) of the
-// context's memory, minus the resident base cache and 256 MB of scratch.
+// context's memory, minus the resident base cache and 256 MB of scratch --
+// and never more than the device can still give this context: its free
+// memory now plus what the context's MSM buffers already hold (they regrow in
+// place), less 2 % of the device for the allocator's granularity.  The second
+// bound accounts for what the first cannot see: prepared bases and scalars the
+// caller keeps resident (68.7 + 17.2 GB for a 2^29 MSM), other contexts'
+// workspaces, other processes.
 template <class C>
 double msm_mem_budget(const ecg_ctx* ctx) {
   double cached = 0;
   for (const auto& e : ctx->base_cache) cached += (double)e.n * msm_base_record_bytes<C>();  // prepared entries
-  return (double)ctx_mem(ctx) * (1.0 - MSM_MEMORY_PADDING) - cached - 256.0 * (1 << 20);
+  const double budget = (double)ctx_mem(ctx) * (1.0 - MSM_MEMORY_PADDING) - cached - 256.0 * (1 << 20);
+  size_t dev_free = 0, dev_total = 0;
+  if (hipMemGetInfo(&dev_free, &dev_total) != hipSuccess) {
+    (void)hipGetLastError();
+    return budget;
+  }
+  double held = 0;
+  for (const auto& kv : ctx->ws)
+    if (kv.first.compare(0, 4, "msm_") == 0) held += (double)kv.second.bytes;
+  const double avail = (double)dev_free + held - 0.02 * (double)dev_total - 256.0 * (1 << 20);
+  return avail < budget ? avail : budget;
 }
 
 template <class C>

@@ -522,6 +522,38 @@ def test_msm_kat_2p24_headline_plan(gpu_programs, cname, cid):
         buf.free()
 
 
+@pytest.mark.timeout(900)
+def test_msm_kat_2p29_two_device_passes():
+    """Above one device pass: 2^29 prepared BLS12-381 bases (68.7 GB of
+    records) and device-resident scalars run as two passes sharing one
+    reduction, 6.9e9 sort entries over 13 windows (every entry index above
+    2^32) -- against the known answer, twice on one context (the first call
+    grows the workspace, the second runs on it; profiles/r06/msm_big/).  The
+    reference's calc_chunk_size splits the same way (multiexp.rs:71-93).  Own
+    program, closed after, so no other test's workspace shares the card."""
+    cname, cid = "bls12_381", 0
+    cv = po.CURVES[cname]
+    n = 1 << 29
+    a, b = 0x29292929, 0x5A5A5
+    E = np.concatenate([rand_scalars_np(cv, 1 << 26, 2900 + i) for i in range(8)])
+    prog = ecgpu.program(ecgpu.Device(0))
+    try:
+        d_e = ecgpu.DeviceBuffer.upload(prog, E)
+        raw = ecgpu.gen_bases_dev(prog, cname, a, b, n)
+        prep = ecgpu.prepare_bases(prog, cname, raw, n)
+        raw.free()
+        first = ecgpu.msm_dev(prog, cname, prep, d_e, n)
+        second = ecgpu.msm_dev(prog, cname, prep, d_e, n)
+        assert normalised_form_ok(cid, first)
+        assert (first == second).all()
+        kat = co.kat_scalar(cid, a, b, E, nthreads=16)
+        assert same_point(cid, first, co.gen_mul(cid, kat))
+        prep.free()
+        d_e.free()
+    finally:
+        prog.close()
+
+
 PINNED = [pytest.param(name, cid, n, id=f"{name}-n{n}") for name, cid in CURVES
           for n in ((1 << 16) + 37, 1 << 17)]
 
