@@ -78,7 +78,9 @@ int ecg_ctx_synchronize(ecg_ctx *ctx);
 /* MSM terms per device pass -- SingleMultiexpKernel::n as calc_chunk_size
  * derives it from Device::memory (multiexp.rs:71-93,109-127): the engine's
  * per-term workspace against (1 - MEMORY_PADDING) of the device memory minus
- * the resident base cache.  Longer MSMs run as several passes, the abort
+ * the resident base cache, and at most the device's free memory at the call
+ * plus the context's own MSM buffers (so buffers the caller keeps resident,
+ * other contexts and other processes shrink it).  Longer MSMs run as several passes, the abort
  * callback polled before each (multiexp.rs:140-144,348-361).
  * ecg_ctx_set_msm_chunk pins it (1 .. 2^31-1; 0 restores the derived value). */
 int ecg_msm_chunk_size(ecg_ctx *ctx, int curve_id, size_t *out_terms);
