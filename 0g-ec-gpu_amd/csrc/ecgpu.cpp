@@ -990,6 +990,17 @@ int ecg_ctx_set_mem_limit(ecg_ctx* ctx, size_t bytes) {
   return ECG_OK;
 }
 
+int ecg_ctx_release_workspace(ecg_ctx* ctx) {
+  ECG_ENTER(ctx);
+  // queued work on any stream may still use a buffer (pick_stream): drain the device
+  ECG_HIP(hipDeviceSynchronize());
+  for (auto& kv : ctx->ws)
+    if (kv.second.ptr) ECG_HIP(hipFree(kv.second.ptr));
+  ctx->ws.clear();
+  ctx->tw_fid = -1;  // the NTT's twiddle tables lived in the workspace
+  return ECG_OK;
+}
+
 int ecg_ctx_set_msm_chunk(ecg_ctx* ctx, size_t max_terms) {
   ECG_ENTER(ctx);
   if (max_terms > 0x7fffffffull) {

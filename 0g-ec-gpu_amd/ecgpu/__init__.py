@@ -122,6 +122,7 @@ _SIGS = {
     "ecg_msm_chunk_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
     "ecg_ctx_set_msm_chunk": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
     "ecg_ctx_set_mem_limit": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "ecg_ctx_release_workspace": (ctypes.c_int, [ctypes.c_void_p]),
     "ecg_ec_fft_set_radix": (ctypes.c_int, [ctypes.c_int]),
     "ecg_comm_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                      ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_size_t,
@@ -370,6 +371,11 @@ class Program:
         """Cap the memory this context plans with and allocates as scratch
         (ecg_ctx_set_mem_limit; 0 = the device's memory)."""
         _check(lib().ecg_ctx_set_mem_limit(self.handle, int(nbytes)), "set_mem_limit")
+
+    def release_workspace(self):
+        """Free this context's device scratch and cached twiddle tables
+        (ecg_ctx_release_workspace); later calls regrow what they need."""
+        _check(lib().ecg_ctx_release_workspace(self.handle), "release_workspace")
 
     def kernel_time(self, name: str) -> tuple[float, int]:
         ms = ctypes.c_double()

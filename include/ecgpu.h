@@ -91,6 +91,15 @@ int ecg_ctx_set_msm_chunk(ecg_ctx *ctx, size_t max_terms);
  * fails with ECG_ERR_NOMEM.  For ranks or provers that share one GPU, as the
  * reference's MEMORY_PADDING leaves room for other users (multiexp.rs:24). */
 int ecg_ctx_set_mem_limit(ecg_ctx *ctx, size_t bytes);
+/* Free the context's device workspace (the grow-only scratch of its MSMs,
+ * NTTs and EC-FFTs, and the cached twiddle tables) after draining the device;
+ * the next call regrows what it needs.  The reference frees its buffers when
+ * a Program / CudaWorkspace is dropped (ag-cuda-proxy/src/module.rs:23-42);
+ * here a long-lived context hands the memory back without being destroyed,
+ * e.g. before one transform that needs most of the 288 GB (a 2^32 NTT: data
+ * plus scratch, 275 GB).  Prepared bases, the base cache and device buffers
+ * the caller allocated are not touched. */
+int ecg_ctx_release_workspace(ecg_ctx *ctx);
 /* "hip=<version> (<libamdhip64 path>); rccl=<version> (<librccl path>)": the
  * HIP runtime and RCCL this process actually bound (launchers check it is the
  * ROCm install's, not another copy loaded earlier into the process). */

@@ -92,6 +92,7 @@ extern "C" {
     pub fn ecg_msm_chunk_size(ctx: *mut ecg_ctx, curve_id: c_int, out_terms: *mut usize) -> c_int;
     pub fn ecg_ctx_set_msm_chunk(ctx: *mut ecg_ctx, max_terms: usize) -> c_int;
     pub fn ecg_ctx_set_mem_limit(ctx: *mut ecg_ctx, bytes: usize) -> c_int;
+    pub fn ecg_ctx_release_workspace(ctx: *mut ecg_ctx) -> c_int;
     pub fn ecg_runtime_info() -> *const c_char;
     pub fn ecg_last_error() -> *const c_char;
     pub fn ecg_version() -> *const c_char;

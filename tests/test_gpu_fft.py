@@ -239,6 +239,7 @@ def test_fft_2p31_2p32_sparse_spot_outputs(gpu_programs, log_n):
     a = np.zeros((n, 4), dtype=np.uint64)
     a[pos] = co.u64arr([f.to_mont(v) for v in vals], 4)
     w = f.omega(n)
+    gpu_programs[0][0].release_workspace()  # data + scratch take 275 GB of the 288: hand back the shared scratch
     prog = ecgpu.program(gpu_programs[1][0])  # its own context: 137 GB of workspace, released below
     try:
         ecgpu.FftKernel.create([prog], "bls12_381_fr").radix_fft(a, co.u64arr([f.to_mont(w)], 4)[0], log_n)

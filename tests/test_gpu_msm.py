@@ -523,7 +523,7 @@ def test_msm_kat_2p24_headline_plan(gpu_programs, cname, cid):
 
 
 @pytest.mark.timeout(900)
-def test_msm_kat_2p29_two_device_passes():
+def test_msm_kat_2p29_two_device_passes(gpu_programs):
     """Above one device pass: 2^29 prepared BLS12-381 bases (68.7 GB of
     records) and device-resident scalars run as two passes sharing one
     reduction, 6.9e9 sort entries over 13 windows (every entry index above
@@ -536,6 +536,7 @@ def test_msm_kat_2p29_two_device_passes():
     n = 1 << 29
     a, b = 0x29292929, 0x5A5A5
     E = np.concatenate([rand_scalars_np(cv, 1 << 26, 2900 + i) for i in range(8)])
+    gpu_programs[0][0].release_workspace()  # the shared context's scratch from earlier tests
     prog = ecgpu.program(ecgpu.Device(0))
     try:
         d_e = ecgpu.DeviceBuffer.upload(prog, E)

@@ -31,6 +31,13 @@ def rand_scalars(cv, n, seed):
     return co.u64arr([rng.field_element(cv.fr) for _ in range(n)], 4)
 
 
+def rand_mont(f, n, seed):
+    """n values < 2^(bits-1) < r: valid Montgomery forms."""
+    a = np.random.default_rng(seed).integers(0, 2**64, size=(n, 4), dtype=np.uint64)
+    a[:, 3] &= np.uint64((1 << (f.bits - 192 - 1)) - 1)
+    return a
+
+
 def same(cid, a, b):
     x, y = co.jac_to_affine(cid, a), co.jac_to_affine(cid, b)
     return (x is None and y is None) or (x is not None and y is not None and (x == y).all())
@@ -261,3 +268,33 @@ def test_msm_multi_pass(progs, cname, cid):
         p.set_msm_chunk(0)
         progs[2].set_msm_chunk(0)
     assert p.msm_chunk_size(cname) > 1 << 26
+
+
+def test_release_workspace_then_rerun(progs):
+    """ecg_ctx_release_workspace frees a context's scratch and its cached
+    twiddle tables: the same NTT and MSM afterwards regrow them and return the
+    same bytes (the tables are rebuilt, not read from freed memory)."""
+    p = progs[0]
+    f = po.BLS12_381_FR
+    log_n = 16
+    a = rand_mont(f, 1 << log_n, 77)
+    w = co.u64arr([f.to_mont(f.omega(1 << log_n))], 4)[0]
+    fk = ecgpu.FftKernel.create([p], "bls12_381_fr")
+    x0 = a.copy()
+    fk.radix_fft(x0, w, log_n)
+    cv = po.CURVES["bn254"]
+    n = 1 << 14
+    B = co.gen_bases(1, 31, 7, n, 8)
+    E = rand_scalars(cv, n, 32)
+    d_b = ecgpu.DeviceBuffer.upload(p, B)
+    d_e = ecgpu.DeviceBuffer.upload(p, E)
+    m0 = ecgpu.msm_dev(p, "bn254", d_b, d_e, n)
+    p.release_workspace()
+    p.release_workspace()  # twice: nothing left to free
+    x1 = a.copy()
+    fk.radix_fft(x1, w, log_n)
+    assert (x1 == x0).all()
+    assert same(1, ecgpu.msm_dev(p, "bn254", d_b, d_e, n), m0)
+    d_b.free()
+    d_e.free()
+
