@@ -1068,6 +1068,105 @@ static uint32_t offset_bits_k(uint32_t S) {
   return std::min(32u, std::max(2u, k));
 }
 
+// 6b'. Offset-bit sums by a merge tree (one-task MSMs; the default in place
+//     of msm_offset_bits_kernel).  Step 5 leaves per window and segment s < S
+//     the partial P_s = sum_j (j + 1) S_{s LS + j} and the run R_s; the window
+//     sum is A + LS sum_k 2^k T_k with A = sum_s P_s and T_k = sum_{s : bit k
+//     of s set} R_s (step 6b; msm_host_fold_bits folds it).  Level j of the
+//     tree holds, per block of 2^j consecutive segments, the block's SP = sum
+//     P, SR = sum R and T_0 .. T_{j-1}; blocks L, R (R's segments above L's)
+//     merge into
+//        SP = SP_L + SP_R,  SR = SR_L + SR_R,  T_k = T_k^L + T_k^R (k < j),
+//        T_j = SR_R:
+//     j + 2 independent adds, one thread (or lane group) each, so every level
+//     is ONE add deep: log2 S levels, ~3 S adds per window.  The bit-sum trees
+//     of msm_offset_bits_kernel did KB S / 2 + S adds, K + 8 deep (24 at 2^20,
+//     40 at 2^26).  Level j block t of window w: comps[(w nblk_j + t) (j + 2) +
+//     i] = SP, SR, T_0, ...  The last level writes the host layout instead:
+//     window w's T_0 .. T_{kb-1}, A at w (kb + 1) (the root's SR is not needed).
+//     The upper levels have few adds, each a latency-bound chain under one wave
+//     per SIMD: there a lane pair or quad shares each add (pp_add).
+//     ECG_MSM_BITS_TREE=0 keeps msm_offset_bits_kernel (A/B).
+static bool msm_bits_tree() {
+  static const bool v = env_u32("ECG_MSM_BITS_TREE", 1) != 0;
+  return v;
+}
+static uint32_t msm_bits_tree_lanes() {  // A/B: ECG_MSM_TREE_LANES = 1 (no sharing), 2 (up to pairs), 4 (up to quads)
+  static const uint32_t v = env_u32_in("ECG_MSM_TREE_LANES", 4, 1, 4);
+  return v;
+}
+
+// level 0 -> 1: segment pairs (2t, 2t + 1) of every window
+template <class F>
+__global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
+    msm_bits_leaf_kernel(const XYZZ<F>* __restrict__ partial, const XYZZ<F>* __restrict__ runs, uint32_t G,
+                         uint32_t S, uint32_t fin, XYZZ<F>* __restrict__ out) {
+  const uint32_t nb1 = (S + 1) / 2;
+  const size_t id = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (size_t)G * nb1 * 2) return;
+  const uint32_t comp = (uint32_t)(id & 1);  // 0: SP, 1: SR (and T_0)
+  const size_t bt = id >> 1;
+  const uint32_t w = (uint32_t)(bt / nb1), t = (uint32_t)(bt % nb1);
+  const XYZZ<F>* src = (comp ? runs : partial) + (size_t)w * S + 2 * t;
+  const XYZZ<F> l = load_xyzz(src);
+  const bool has_r = 2 * t + 1 < S;
+  const XYZZ<F> r = has_r ? load_xyzz(src + 1) : xyzz_zero<F>();
+  if (fin) {  // S = 2: [T_0, A]
+    if (comp == 0)
+      store_xyzz(&out[(size_t)w * 2 + 1], has_r ? pa_add(l, r) : l);
+    else
+      store_xyzz(&out[(size_t)w * 2], r);
+    return;
+  }
+  XYZZ<F>* o = out + bt * 3;
+  store_xyzz(&o[comp], has_r ? pa_add(l, r) : l);
+  if (comp == 1) store_xyzz(&o[2], r);  // T_0 = R_{2t+1}
+}
+
+// level j -> j + 1 (j >= 1): one add per (window, output block, component),
+// on 2^LB lanes (PM: pp_add's lane sharing; LB = pp_lanes_log<PM>())
+template <class F, int PM>
+__global__ void __launch_bounds__(MSM_THREADS) ECG_RED_ATTR
+    msm_bits_merge_kernel(const XYZZ<F>* __restrict__ in, uint32_t G, uint32_t nblk_in, uint32_t j, uint32_t fin,
+                          XYZZ<F>* __restrict__ out) {
+  constexpr uint32_t LB = pp_lanes_log<PM>();
+  const uint32_t nblk_out = (nblk_in + 1) / 2, ci = j + 2;
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t id = gid >> LB;  // the lanes of one add leave together
+  if (id >= (size_t)G * nblk_out * ci) return;
+  const bool lead = (gid & ((1u << LB) - 1)) == 0;
+  const uint32_t comp = (uint32_t)(id % ci);
+  const size_t bt = id / ci;  // (w, t) of the output block
+  const uint32_t t = (uint32_t)(bt % nblk_out), w = (uint32_t)(bt / nblk_out);
+  if (fin && comp == 1) {  // the root's SR is not needed, only T_j = SR_R
+    if (lead) {
+      const bool has_r = 2 * t + 1 < nblk_in;
+      const XYZZ<F> r = has_r ? load_xyzz(&in[((size_t)w * nblk_in + 2 * t + 1) * ci + 1]) : xyzz_zero<F>();
+      store_xyzz(&out[(size_t)w * (j + 2) + j], r);
+    }
+    return;
+  }
+  const XYZZ<F>* L = in + ((size_t)w * nblk_in + 2 * t) * ci;
+  const bool has_r = 2 * t + 1 < nblk_in;  // uniform over the add's lanes
+  const XYZZ<F> l = load_xyzz(&L[comp]);
+  XYZZ<F> v = l, r = xyzz_zero<F>();
+  if (has_r) {
+    r = load_xyzz(&L[ci + comp]);
+    v = pp_add<PM>(l, r);
+  }
+  // every lane of the group stores the same point: a lane-0-only store let
+  // the compiler sink the lane exchanges of the result past the branch (the
+  // G2 quad form returned a wrong point there, tests/test_gpu_g2.py)
+  if (fin) {  // host layout [T_0 .. T_j, A]
+    XYZZ<F>* o = out + (size_t)w * (j + 2);
+    store_xyzz(&o[comp == 0 ? j + 1 : comp - 2], v);
+  } else {
+    XYZZ<F>* o = out + bt * (j + 3);
+    store_xyzz(&o[comp], v);
+    if (comp == 1) store_xyzz(&o[j + 2], r);  // T_j = SR_R
+  }
+}
+
 // A few points per group (batched MSMs: 2 reduction segments per (task,
 // window)): one thread per group adds them serially.  A tree-sum workgroup per
 // group would run 8 LDS levels of adds for 2 inputs (13.9 ms on the AMT shape,
@@ -1157,7 +1256,7 @@ __global__ void __launch_bounds__(64)
     for (uint32_t k = 0; k < c; k++) acc = pp_dbl<PM>(acc);
     acc = pp_add<PM>(acc, load_xyzz(&sums[(size_t)t * nw + w]));
   }
-  if ((g & ((1u << PB) - 1)) == 0) store_xyzz(&out[t], acc);
+  store_xyzz(&out[t], acc);  // every lane of the task holds acc (see msm_bits_merge_kernel)
 }
 static uint32_t msm_fold_lanes() {  // A/B: ECG_MSM_FOLD_PAIRS = 0 / 1 (one lane per task), 2 (pairs), 4 (quads)
   static const uint32_t v = env_u32_in("ECG_MSM_FOLD_PAIRS", 4, 0, 4);
@@ -1343,8 +1442,10 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   MsmPlan pl = pl0;  // reduction segments sized for this point form's occupancy
   plan_reduction(pl, RedWaves<F>::value);
   // one-task MSMs leave per window the A sum and the KB offset-bit sums
-  // (msm_offset_bits_kernel, folded on the host); batched ones the window sums
+  // (the merge tree, or msm_offset_bits_kernel; folded on the host); batched
+  // ones the window sums
   const bool bits = folded == nullptr;
+  const bool tree = bits && msm_bits_tree() && pl.S >= 2;  // offset-bit sums by the merge tree (6b')
   const bool do_acc = phase == CORE_ALL || phase == CORE_ACC, do_fin = phase == CORE_ALL || phase == CORE_FIN;
   const size_t m = (size_t)g.n_chunks * g.clen;  // scalars consumed
   const uint32_t nb = pl.G * pl.B;
@@ -1383,6 +1484,16 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     long_runs = (uint32_t*)((char*)bk_all + (size_t)nslots * nb * sizeof(X));
   }
   ECG_TRY(ws_get(ctx, "msm_pa", (size_t)pl.G * pl.S * sizeof(X), &pa));
+  // the merge tree's levels (6b'): odd ones in msm_tree1 (level 1, 3 points per
+  // segment pair, is the largest), even ones in msm_tree2 (level 2: 4 points
+  // per 4 segments); either may hold the last level's G (kb + 1) sums.  Every
+  // phase sizes them.
+  void *t1 = nullptr, *t2 = nullptr;
+  if (tree) {
+    const size_t fin_pts = (size_t)pl.G * (offset_bits(pl.S) + 1);
+    ECG_TRY(ws_get(ctx, "msm_tree1", std::max((size_t)pl.G * ((pl.S + 1) / 2) * 3, fin_pts) * sizeof(X), &t1));
+    ECG_TRY(ws_get(ctx, "msm_tree2", std::max((size_t)pl.G * ((pl.S + 3) / 4) * 4, fin_pts) * sizeof(X), &t2));
+  }
   const uint32_t tree_span = MSM_TREE_K * MSM_THREADS;  // inputs per tree-sum workgroup
   ECG_TRY(ws_get(ctx, "msm_pb", ((size_t)pl.G * ((pl.S + tree_span - 1) / tree_span) + pl.G) * sizeof(X), &pb));
   // sort geometry (section 2 below)
@@ -1541,11 +1652,6 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
   }  // do_acc
   if (!do_fin) return ECG_OK;
 
-  void* runs;
-  ECG_TRY(ws_get(ctx, "msm_runs", (size_t)pl.G * pl.S * sizeof(X), &runs));
-  hipLaunchKernelGGL(msm_reduce_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
-                     dim3(MSM_THREADS), 0, s, (const X*)bk_all, pl, (X*)pa, (X*)runs, nslots, (size_t)nb);
-  ECG_HIP(hipGetLastError());
   uint32_t cnt = pl.S;
   uint32_t groups = pl.G;
   X* in = (X*)pa;
@@ -1557,7 +1663,53 @@ int msm_core_impl(ecg_ctx* ctx, const void* d_bases, const void* d_scalars, cons
     ECG_HIP(hipFuncSetAttribute((const void*)msm_offset_bits_kernel<F>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)tree_lds));
   }
-  if (bits) {
+  void* runs;
+  ECG_TRY(ws_get(ctx, "msm_runs", (size_t)pl.G * pl.S * sizeof(X), &runs));
+  hipLaunchKernelGGL(msm_reduce_kernel<F>, dim3(blocks_for((size_t)pl.G * pl.S, MSM_THREADS)),
+                     dim3(MSM_THREADS), 0, s, (const X*)bk_all, pl, (X*)pa, (X*)runs, nslots, (size_t)nb);
+  ECG_HIP(hipGetLastError());
+  if (tree) {
+    const uint32_t kb = offset_bits(pl.S);
+    X* lv[2] = {(X*)t1, (X*)t2};
+    uint32_t nblk = (pl.S + 1) / 2;
+    hipLaunchKernelGGL(msm_bits_leaf_kernel<F>, dim3(blocks_for((size_t)pl.G * nblk * 2, MSM_THREADS)),
+                       dim3(MSM_THREADS), 0, s, (const X*)pa, (const X*)runs, pl.G, pl.S, kb == 1 ? 1u : 0u,
+                       lv[0]);
+    ECG_HIP(hipGetLastError());
+    int cur = 0;
+    for (uint32_t j = 1; j < kb; j++) {
+      const uint32_t nout = (nblk + 1) / 2;
+      const size_t adds = (size_t)pl.G * nout * (j + 2);
+      const uint32_t fin = j + 1 == kb ? 1u : 0u;
+      // share each add over a lane quad / pair while that keeps the level
+      // under one wave per SIMD (1024 SIMDs x 64 lanes)
+      const uint32_t lanes = msm_bits_tree_lanes();
+      bool done = false;
+      if constexpr (QuadOps<F>::ok) {
+        if (lanes >= 4 && adds * 4 <= 1024u * 64u) {
+          hipLaunchKernelGGL((msm_bits_merge_kernel<F, 4>), dim3(blocks_for(adds * 4, MSM_THREADS)), dim3(MSM_THREADS),
+                             0, s, (const X*)lv[cur], pl.G, nblk, j, fin, lv[cur ^ 1]);
+          done = true;
+        }
+      }
+      if constexpr (PairOps<F>::ok) {
+        if (!done && lanes >= 2 && adds * 2 <= 1024u * 64u) {
+          hipLaunchKernelGGL((msm_bits_merge_kernel<F, 1>), dim3(blocks_for(adds * 2, MSM_THREADS)), dim3(MSM_THREADS),
+                             0, s, (const X*)lv[cur], pl.G, nblk, j, fin, lv[cur ^ 1]);
+          done = true;
+        }
+      }
+      if (!done)
+        hipLaunchKernelGGL((msm_bits_merge_kernel<F, 0>), dim3(blocks_for(adds, MSM_THREADS)), dim3(MSM_THREADS), 0, s,
+                           (const X*)lv[cur], pl.G, nblk, j, fin, lv[cur ^ 1]);
+      ECG_HIP(hipGetLastError());
+      cur ^= 1;
+      nblk = nout;
+    }
+    in = lv[cur];  // per window T_0 .. T_{kb-1}, A
+    groups = pl.G * (kb + 1);
+    cnt = 1;
+  } else if (bits) {
     const uint32_t kb = offset_bits(pl.S);
     const uint32_t K = offset_bits_k(pl.S);
     const uint32_t wgs = (pl.S + MSM_THREADS * K - 1) / (MSM_THREADS * K);
@@ -1835,13 +1987,14 @@ int msm_prepare_t(ecg_ctx* ctx, const void* d_bases, size_t n, uint32_t tab_c, v
 // per window the A sum and offset_bits(S) bit sums (msm_offset_bits_kernel).
 template <class C>
 MsmPlan msm_eff_plan(MsmPlan pl) {
+  bool done = false;
   if constexpr (MsmField<C>::rr) {
     if (msm_rr_enabled()) {
       plan_reduction(pl, RedWaves<typename MsmField<C>::type>::value);
-      return pl;
+      done = true;
     }
   }
-  plan_reduction(pl, RedWaves<typename C::Fq>::value);
+  if (!done) plan_reduction(pl, RedWaves<typename C::Fq>::value);
   return pl;
 }
 static inline uint32_t msm_single_sums(const MsmPlan& e) { return e.G * (offset_bits(e.S) + 1); }
