@@ -981,6 +981,10 @@ int ecg_gen_bases_dev(ecg_ctx* ctx, int curve_id, const uint64_t* a, const uint6
     set_error("ecg_gen_bases_dev: null pointer");
     return ECG_ERR_INVALID;
   }
+  if (!(b[0] | b[1] | b[2] | b[3])) {  // the generator steps by bG: b = 0 would step by the identity
+    set_error("ecg_gen_bases_dev: b must be non-zero (the bases step by b G; upload equal bases instead)");
+    return ECG_ERR_INVALID;
+  }
   return gen_bases_run(ctx, curve_id, a, b, n, d_out, pick_stream(ctx, stream));
 }
 

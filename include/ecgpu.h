@@ -467,7 +467,8 @@ int ecg_dev_download(ecg_ctx *ctx, void *dst, const void *d_src, size_t bytes);
 
 /* ---- synthetic inputs for benchmarks/tests (not part of the reference API)
  * Bases P_i = (a + i*b) * G for i < n written to device memory d_out
- * (n x 2 x Lq u64, GpuRepr layout); a, b canonical 4-limb scalars. */
+ * (n x 2 x Lq u64, GpuRepr layout); a, b canonical 4-limb scalars, b != 0
+ * (ECG_ERR_INVALID otherwise: the generator steps by b G). */
 int ecg_gen_bases_dev(ecg_ctx *ctx, int curve_id, const uint64_t *a, const uint64_t *b, size_t n,
                       void *d_out, void *stream);
 

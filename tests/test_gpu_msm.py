@@ -678,3 +678,77 @@ def test_msm_boundary_form_pipeline(gpu_programs, cname, cid, tmp_path):
     for p in outs[1:]:
         co.lib().orc_jac_add(cid, co.ptr(acc), co.ptr(acc), co.ptr(np.ascontiguousarray(p)))
     assert same_point(cid, acc, want)
+
+
+_TREE_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import ecgpu
+cname, path_e, a, b, path_b = sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]), sys.argv[6]
+E = np.load(path_e)
+n = E.shape[0]
+prog = ecgpu.program(ecgpu.Device(0))
+d_b = ecgpu.DeviceBuffer.upload(prog, np.load(path_b)) if path_b else ecgpu.gen_bases_dev(prog, cname, a, b, n)
+d_e = ecgpu.DeviceBuffer.upload(prog, E)
+outs = [ecgpu.msm_dev(prog, cname, d_b, d_e, n)]
+outs += [ecgpu.msm_grid_part(prog, cname, d_b, d_e, n, r, 2)[0] for r in range(2)]
+for o in outs:
+    print(" ".join("%x" % int(v) for v in o))
+"""
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("cname,cid", CURVES)
+def test_msm_bits_tree_matches_offset_kernel(gpu_programs, cname, cid, tmp_path):
+    """The offset-bit sums by the merge tree (the default, lane quads on its
+    upper levels) against the same MSMs through msm_offset_bits_kernel
+    (ECG_MSM_BITS_TREE=0) and through the tree on single lanes
+    (ECG_MSM_TREE_LANES=1), in child processes: a single MSM and a 2-rank grid
+    split at 2^18 (the tree's top levels on quads), with uniform and all-ones
+    scalars, and with all bases equal (equal bucket sums drive the adds'
+    doubling branch), each against the known answer."""
+    import subprocess
+
+    cv = po.CURVES[cname]
+    n = 1 << 18
+    a, b = 0x7EE5, 0x3
+    prog = gpu_programs[0][0]
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "0g-ec-gpu_amd")
+    ones = np.zeros((n, 4), dtype=np.uint64)
+    ones[:, 0] = 1
+    uni = rand_scalars_np(cv, n, 1818 + cid)
+    # all bases equal (aG, uploaded): bucket sums are count x aG, so equal
+    # counts make equal points in the running sums and the tree's merges
+    pb = str(tmp_path / "b_equal.npy")
+    np.save(pb, np.ascontiguousarray(np.tile(co.gen_bases(cid, a, 1, 1)[0], (n, 1))))
+    for tag, E, bb, path_b in (("uniform", uni, b, ""), ("ones", ones, b, ""), ("equal_bases", uni, 0, pb)):
+        pe = str(tmp_path / f"e_{tag}.npy")
+        np.save(pe, E)
+        d_b = ecgpu.DeviceBuffer.upload(prog, np.load(path_b)) if path_b else ecgpu.gen_bases_dev(prog, cname, a, bb, n)
+        d_e = ecgpu.DeviceBuffer.upload(prog, E)
+        here = ecgpu.msm_dev(prog, cname, d_b, d_e, n)
+        assert same_point(cid, here, co.gen_mul(cid, co.kat_scalar(cid, a, bb, E, nthreads=16))), tag
+        for env in ({"ECG_MSM_BITS_TREE": "0"}, {"ECG_MSM_TREE_LANES": "1"}):
+            res = subprocess.run([sys.executable, "-c", _TREE_CHILD, pkg, cname, pe, str(a), str(bb), path_b],
+                                 env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
+            assert res.returncode == 0, res.stderr[-2000:]
+            outs = [np.array([int(x, 16) for x in ln.split()], dtype=np.uint64)
+                    for ln in res.stdout.split("\n") if ln.strip()]
+            assert len(outs) == 3, (tag, env)
+            assert same_point(cid, outs[0], here), (tag, env)
+            nq = ecgpu.CURVE_FQ_LIMBS[cid]
+            acc = np.zeros(3 * nq, dtype=np.uint64)
+            for p in outs[1:]:
+                co.lib().orc_jac_add(cid, co.ptr(acc), co.ptr(acc), co.ptr(np.ascontiguousarray(p)))
+            assert same_point(cid, acc, here), (tag, env)
+        d_e.free()
+        d_b.free()
+
+
+def test_gen_bases_rejects_zero_step(gpu_programs):
+    """The synthetic-base generator steps by b G: b = 0 is refused (it once
+    returned garbage points, which the equal-bases case above now uploads)."""
+    prog = gpu_programs[0][0]
+    with pytest.raises(ecgpu.EcError, match="b must be non-zero"):
+        ecgpu.gen_bases_dev(prog, "bls12_381", 5, 0, 16)
+
